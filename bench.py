@@ -1,0 +1,303 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident batched Internet checksum on MI355X (BASELINE.json metric).
+
+A "step" = one launch of the hot path over one batch. Headline workload (N=1) is
+BASELINE config 3 — 1M x 1500-byte TCP segments including the pseudo-header, the
+configuration the north-star target (>=70 % of HBM peak) is quoted on; with
+--gpus N every rank processes its own 1M-segment shard (config 5 = 8 x config 3,
+weak scaling, no data-path collective — packets are independent).
+
+value      = algorithmic bytes of all ranks / max-over-ranks wall time, in GiB/s
+             (payload + per-packet side arrays + uint16 results)
+roofline   = the dominant (only) kernel's algorithmic bytes / its average launch
+             duration from HIP events on its stream, vs 8.0 TB/s HBM peak
+cpu_baseline = the C restatement of checksum.go (oracle/, "port", reference-faithful
+             -O2 -fno-tree-vectorize) on host cores over a bounded sample of the
+             same batch (rank 0, N=1 only); the same leg checks the GPU results
+             of the timed batch bit-for-bit against it.
+
+Run: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from yustack_amd import batch  # noqa: E402
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+N_PKT = 1 << 20
+ROTATE_MIN_BYTES = 2 << 30  # rotate batches so each step streams from HBM, not the 256 MiB MALL
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class Workload:
+    """One BASELINE config, materialised on the device with R rotating copies."""
+
+    def __init__(self, cfg: int, dev: torch.device, seed: int):
+        self.cfg = cfg
+        self.dev = dev
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        n = N_PKT
+        self.n = n
+        self.offsets = None
+        self.initial_arr = None
+        self.addrs = None
+        if cfg == 2:  # 1M x 64-B UDP payloads: A1 over the payload, pseudo-header partial as initial
+            self.mode, self.L = batch.RAW, 64
+            nbytes = n * self.L
+            self.side = 2 * n  # uint16 initial
+            self.name = "config2: 1M x 64-B UDP payloads, Checksum(payload, pseudo) per packet"
+        elif cfg == 3:  # 1M x 1500-B TCP segments, (src,dst) side array
+            self.mode, self.L = batch.TCP, 1500
+            nbytes = n * self.L
+            self.side = 8 * n  # addrs
+            self.name = "config3: 1M x 1500-B TCP segments incl. pseudo-header (sendTCP field value)"
+        elif cfg == 4:  # ragged 64..9000 B, back-to-back, RAW with initial
+            self.mode = batch.RAW
+            rng = np.random.default_rng(4)
+            lens = rng.integers(64, 9001, size=n)
+            offs = np.zeros(n + 1, dtype=np.int64)
+            offs[1:] = np.cumsum(lens)
+            nbytes = int(offs[-1])
+            self.L = 0
+            self.offsets = torch.from_numpy(offs).to(dev)
+            self.side = 8 * (n + 1) + 2 * n
+            self.name = "config4: ragged 1M packets U{64..9000} B back-to-back (odd offsets), one wave per packet"
+        else:
+            raise SystemExit(f"unknown config {cfg}")
+        self.payload = nbytes
+        self.R = max(1, -(-ROTATE_MIN_BYTES // nbytes))
+        self.data = []
+        for _ in range(self.R):
+            d = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=dev, generator=g)
+            if cfg == 3:  # 20-B header: DataOffset 5, checksum field 0 (Encode)
+                v = d.view(n, self.L)
+                v[:, 12] = 0x50
+                v[:, 16:18] = 0
+            self.data.append(d)
+        if cfg == 2 or cfg == 4:
+            self.initial_arr = torch.randint(0, 65536, (n,), dtype=torch.int32, device=dev,
+                                             generator=g).to(torch.uint16)
+        if cfg == 3:
+            self.addrs = torch.randint(0, 256, (8 * n,), dtype=torch.uint8, device=dev, generator=g)
+        self.out = torch.empty(n, dtype=torch.uint16, device=dev)
+        if self.offsets is not None:  # validate once; the timed launches skip the check
+            batch.checksum_ragged(self.data[0], self.offsets, self.mode,
+                                  initial_arr=self.initial_arr, out=self.out)
+        # algorithmic bytes per launch: payload + side arrays + uint16 out
+        self.bytes = self.payload + self.side + 2 * n
+
+    def step(self, k: int) -> None:
+        d = self.data[k % self.R]
+        if self.offsets is None:
+            batch.checksum_uniform(d, self.L, self.L, self.n, self.mode, initial_arr=self.initial_arr,
+                                   addrs=self.addrs, out=self.out)
+        else:
+            batch.checksum_ragged(d, self.offsets, self.mode, initial_arr=self.initial_arr,
+                                  out=self.out, validate=False)
+
+    def kernel_name(self) -> str:
+        if self.offsets is not None:
+            return "k_loop<4>"
+        return batch.variant(self.L, self.L, self.mode, self.data[0].data_ptr() & 15)
+
+
+def timed(w: Workload, steps: int, warmup: int, dist: bool):
+    for k in range(warmup):
+        w.step(k)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for k in range(steps):
+        w.step(warmup + k)
+    ev1.record()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    wall = time.perf_counter() - t0
+    kern = ev0.elapsed_time(ev1) / 1e3 / steps  # s per launch, HIP events on the kernel's stream
+    return wall, kern
+
+
+def cpu_baseline(w: Workload, threads: int, budget_s: float):
+    """Oracle ("port") on host cores over a bounded sample; also full-batch parity."""
+    from oracle import oracle as O  # cpu_baseline leg only (test infrastructure)
+    C = O.C()
+    host = w.data[0].cpu().numpy()
+    ia = None if w.initial_arr is None else w.initial_arr.cpu().numpy()
+    ad = None if w.addrs is None else w.addrs.cpu().numpy()
+    offs = None if w.offsets is None else w.offsets.cpu().numpy().view(np.uint64)
+    # full-size parity of the GPU path on data[0]
+    w.step(0)
+    torch.cuda.synchronize()
+    got = w.out.cpu().numpy()
+    if offs is None:
+        want = C.batch(host, w.mode, stride=w.L, length=w.L, n=w.n, initial_arr=ia, addrs=ad, threads=threads)
+    else:
+        want = C.batch(host, w.mode, offsets=offs, initial_arr=ia, threads=threads)
+    parity = bool(np.array_equal(got, want))
+
+    def rate(nthreads, sample_pk):
+        sample_pk = min(sample_pk, w.n)
+        if offs is None:
+            run = lambda: C.batch(host, w.mode, stride=w.L, length=w.L, n=sample_pk, initial_arr=ia,  # noqa: E731
+                                  addrs=ad, threads=nthreads)
+            b = sample_pk * w.L
+        else:
+            o = offs[:sample_pk + 1]
+            run = lambda: C.batch(host, w.mode, offsets=o, initial_arr=ia, threads=nthreads)  # noqa: E731
+            b = int(o[-1] - o[0])
+        b_alg = b + (w.side + 2 * w.n) * sample_pk / w.n
+        reps, t = 0, 0.0
+        t0 = time.perf_counter()
+        while t < budget_s / 2 or reps < 2:
+            run()
+            reps += 1
+            t = time.perf_counter() - t0
+        return reps * b_alg / t / GIB, sample_pk, reps, t
+    r1, s1, n1, t1 = rate(1, 1 << 15)
+    rT, sT, nT, tT = rate(threads, w.n)
+    return parity, {
+        "value": round(rT, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": (f"oracle/csum_oracle.c (literal checksum.go + sendTCP/sendUDP composition, "
+                   f"-O2 -fno-tree-vectorize), static even split over {threads} host threads: "
+                   f"{nT} pass(es) over the first {sT} packets of the timed batch in {tT:.1f} s; "
+                   f"1 thread: {r1:.3f} GiB/s, {n1} pass(es) over {s1} packets in {t1:.1f} s"),
+        "value_1core": round(r1, 3),
+        "cpu_work_s": round(t1 + tT * threads, 1),
+    }
+
+
+def host_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip configs 2/4 side measurements")
+    ap.add_argument("--cpu-budget", type=float, default=6.0, help="wall seconds for the CPU baseline")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    w = Workload(args.config, dev, seed=1000 + rank)
+    wall, kern = timed(w, args.steps, args.warmup, dist)
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    wall_max = float(t.item())
+    ms_per_step = wall_max / args.steps * 1e3
+    value = world * w.bytes * args.steps / wall_max / GIB
+    achieved = w.bytes / kern / 1e9  # GB/s (decimal, like the peak)
+
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(f"config{args.config}")
+        except Exception:
+            traffic = None
+
+    res = {
+        "metric": "GiB/s device-resident Internet checksum, batched packets, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded torch.randint bytes on device; TCP header DataOffset 5, field 0)",
+        "config": {
+            "workload": w.name,
+            "packets_per_gpu": w.n,
+            "packet_bytes": w.L if w.L else "U{64..9000}",
+            "mode": {0: "raw", 2: "tcp"}.get(w.mode, str(w.mode)),
+            "algorithmic_bytes_per_step_per_gpu": w.bytes,
+            "rotating_batches": w.R,
+            "kernel": w.kernel_name(),
+            "parallelism": f"shard{world} (independent packets, no collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel_avg_us": round(kern * 1e6, 2),
+        },
+    }
+
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra = {}
+        for c in (2, 3, 4):
+            if c == args.config:
+                continue
+            wc = Workload(c, dev, seed=77 + c)
+            wl, kc = timed(wc, max(10, args.steps // 2), args.warmup, False)
+            extra[f"config{c}"] = {
+                "GiB_s": round(wc.bytes * max(10, args.steps // 2) / wl / GIB, 2),
+                "kernel_avg_us": round(kc * 1e6, 2),
+                "roofline_frac": round(wc.bytes / kc / 1e9 / HBM_PEAK_GBS, 4),
+                "kernel": wc.kernel_name(),
+            }
+            del wc
+            torch.cuda.empty_cache()
+        res["other_configs"] = extra
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        parity, cb = cpu_baseline(w, host_threads(), args.cpu_budget)
+        res["cpu_baseline"] = cb
+        res["parity_full_batch_vs_oracle"] = parity
+    else:
+        res["cpu_baseline"] = None
+
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

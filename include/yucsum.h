@@ -1,0 +1,209 @@
+/*
+ * yucsum.h — C ABI of the MI355X-native Internet-checksum engine.
+ *
+ * This is the drop-in boundary for yustack's `checksum` package
+ * (reference: /root/reference/checksum/checksum.go). The reference exposes
+ * three package-level Go functions and nothing else; every caller
+ * (header/ipv4.go:177-179, header/tcp.go:165-173, header/udp.go:67-75,
+ * types/route.go:90-92, transport/udp/endpoint.go:175,
+ * transport/tcp/connect.go:314,580, network/ipv4/icmp.go:42,
+ * checker/checker.go:32,84-88) reaches the hot path through them.
+ *
+ * Two groups of entry points:
+ *
+ *  1. Scalar, Go-signature entry points (yu_checksum, yu_checksum_combine,
+ *     yu_pseudo_header_checksum). These are what a cgo shim binds so that the
+ *     reference's callers compile unchanged. They run on the
+ *     calling host thread: a cgo call costs ~100 ns, a GPU round trip costs
+ *     microseconds, so per-call offload would be a pessimisation. They are
+ *     total functions (never fail), reentrant and allocation-free.
+ *
+ *  2. Batched device entry points (yu_csum_batch_uniform,
+ *     yu_csum_batch_ragged). These are the GPU hot path: one launch computes
+ *     the per-packet sums of a whole device-resident batch with hand-written
+ *     gfx950 HIP kernels. They are asynchronous on the given HIP stream,
+ *     perform no allocation and no synchronisation (graph-capturable), and
+ *     return a status code. There is no CPU fallback: without a usable GPU
+ *     they return a negative status.
+ *
+ *  3. Batched host entry point (yu_csum_batch_host_uniform): the path that
+ *     starts and ends in host memory (tun / link-layer buffers). It stages
+ *     through library-owned pinned buffers and overlaps H2D copy, kernel and
+ *     D2H copy on separate streams. Synchronous.
+ *
+ * All arithmetic is unsigned integer. Results are bit-identical to the
+ * reference Go code on the same bytes, including the reference's uint32
+ * wrap-around for buffers longer than 131072 bytes (RAW mode).
+ */
+#ifndef YUCSUM_H
+#define YUCSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YUCSUM_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ */
+/* Status codes (batched entry points).                               */
+/* ------------------------------------------------------------------ */
+#define YU_OK 0
+#define YU_EINVAL (-22)         /* bad argument (mode, NULL pointer, len) */
+#define YU_ENODEV (-19)         /* no HIP device / device index out of range */
+#define YU_ENOMEM (-12)         /* pinned/device staging allocation failed */
+#define YU_EHIP_BASE (-1000)    /* -(1000 + hipError_t) for any other HIP error */
+
+/* ------------------------------------------------------------------ */
+/* Scalar entry points (host CPU, Go-signature drop-ins).             */
+/* ------------------------------------------------------------------ */
+
+/* Replaces `func Checksum(buf []byte, initial uint16) uint16`
+ * (checksum/checksum.go:4-18). Sum of big-endian 16-bit words of buf, odd
+ * trailing byte as the high byte of a final word, plus `initial`, in a
+ * uint32 accumulator that wraps mod 2^32, folded once by ChecksumCombine.
+ * The result is NOT complemented. len==0 (buf may be NULL) returns
+ * fold(initial) == initial. */
+uint16_t yu_checksum(const uint8_t *buf, size_t len, uint16_t initial);
+
+/* Replaces `func ChecksumCombine(a, b uint16) uint16`
+ * (checksum/checksum.go:32-35): one end-around-carry add. */
+uint16_t yu_checksum_combine(uint16_t a, uint16_t b);
+
+/* Replaces `func PseudoHeaderChecksum(protocol uint32, srcAddr, dstAddr
+ * string) uint16` (checksum/checksum.go:24-28). Go strings become
+ * (pointer, length) pairs; the protocol is truncated to uint8 exactly as
+ * `uint8(protocol)` does. The transport length is NOT included (callers add
+ * it through {UDP,TCP}.CalculateChecksum, header/udp.go:67-75,
+ * header/tcp.go:165-173). */
+uint16_t yu_pseudo_header_checksum(uint32_t protocol,
+                                   const uint8_t *src_addr, size_t src_len,
+                                   const uint8_t *dst_addr, size_t dst_len);
+
+/* ------------------------------------------------------------------ */
+/* Batched modes. Each names the reference composition it reproduces.  */
+/* "pseudo" = the per-packet pseudo-header partial sum: either the 8-byte */
+/* {src[4], dst[4]} record from `addrs` (protocol fixed by the mode) or,  */
+/* when addrs is NULL, the uint16 PseudoHeaderChecksum value from        */
+/* `initial_arr[i]` (or the scalar `initial`).                           */
+/* ------------------------------------------------------------------ */
+
+/* out[i] = Checksum(pkt_i, initial_i)  — checksum/checksum.go:4-18.
+ * Uncomplemented; exact for any length (uint32 wrap reproduced). */
+#define YU_MODE_RAW 0
+/* pkt_i = UDP header (8 B) + data. out[i] = the value sendUDP stores:
+ * ^UDP.CalculateChecksum(Checksum(data, pseudo), len) with the header's
+ * checksum field taken as 0 (Encode writes 0) —
+ * transport/udp/endpoint.go:164-187, header/udp.go:67-83. Protocol 17. */
+#define YU_MODE_UDP 1
+/* pkt_i = TCP segment (header incl. options, then data). out[i] = the value
+ * sendTCP stores: ^TCP.CalculateChecksum(Checksum(data, pseudo), len) with
+ * the checksum field taken as 0 — transport/tcp/connect.go:556-586,
+ * header/tcp.go:165-186. Protocol 6. */
+#define YU_MODE_TCP 2
+/* pkt_i = IPv4 datagram. out[i] = ^IPv4.CalculateChecksum() over
+ * b[:IHL*4] (clamped to len) with the header-checksum field taken as 0 —
+ * network/ipv4/ipv4.go:80-97, header/ipv4.go:146-157,177-179. initial and
+ * addrs are ignored. */
+#define YU_MODE_IPV4 3
+/* pkt_i = ICMPv4 message (4-byte header + data). out[i] =
+ * ^Checksum(hdr, Checksum(data, 0)) with the checksum field taken as 0 —
+ * network/ipv4/icmp.go:36-45. initial and addrs are ignored. */
+#define YU_MODE_ICMP 4
+/* Receive-side verification, checker semantics (checker/checker.go:25-40):
+ * out[i] = Checksum(b[:IHL*4], 0) INCLUDING the stored field. The packet is
+ * valid iff out[i] is 0x0000 or 0xFFFF. */
+#define YU_MODE_VERIFY_IPV4 5
+/* checker.TCP (checker/checker.go:71-99): out[i] = Checksum over
+ * pseudo ‖ BE16(len) ‖ segment INCLUDING the stored field. Valid iff
+ * out[i] ∈ {0, 0xFFFF}. Protocol 6. */
+#define YU_MODE_VERIFY_TCP 6
+/* The same verification for UDP datagrams (protocol 17). The reference
+ * never verifies on receive (transport/udp/endpoint.go:191-229); this is
+ * the checker.TCP formula applied to UDP. */
+#define YU_MODE_VERIFY_UDP 7
+#define YU_MODE_COUNT 8
+
+/* Packets handed to the transport/IPv4/ICMP modes must be <= 65535 bytes
+ * (the IPv4 total-length limit; the reference's uint16 length arithmetic is
+ * only defined there). RAW mode accepts any length < 2^32. */
+#define YU_MAX_TRANSPORT_LEN 65535u
+
+/* ------------------------------------------------------------------ */
+/* Batched device entry points (the GPU hot path).                     */
+/* All pointers are device pointers (hipMalloc / torch CUDA tensors).   */
+/* `stream` is a hipStream_t (NULL = legacy default stream).            */
+/* Asynchronous: returns after enqueueing the kernel.                   */
+/* ------------------------------------------------------------------ */
+
+/* Uniform-stride batch: packet i occupies data[i*stride, i*stride + len).
+ * Packets may overlap (stride < len) — they are only read.
+ *  initial_arr: NULL or n uint16 (per-packet initial / pseudo partial)
+ *  initial:     used when initial_arr == NULL
+ *  addrs:       NULL or n*8 bytes {src[4], dst[4]} (UDP/TCP/VERIFY_TCP/UDP)
+ *  out:         n uint16 results, written in host byte order as a number
+ *               (store it big-endian into the packet to set the field). */
+int yu_csum_batch_uniform(const uint8_t *data, uint64_t stride, uint32_t len,
+                          uint64_t n, int mode,
+                          const uint16_t *initial_arr, uint16_t initial,
+                          const uint8_t *addrs, uint16_t *out, void *stream);
+
+/* Ragged batch (tun-style back-to-back packets, any byte alignment):
+ * packet i occupies data[offsets[i], offsets[i+1]); offsets is a device
+ * array of n+1 non-decreasing uint64 (the layout of buffer.VectorisedView
+ * flattened, buffer/view.go:37-46). */
+int yu_csum_batch_ragged(const uint8_t *data, const uint64_t *offsets,
+                         uint64_t n, int mode,
+                         const uint16_t *initial_arr, uint16_t initial,
+                         const uint8_t *addrs, uint16_t *out, void *stream);
+
+/* In-place field writer (TX modes UDP/TCP/IPV4/ICMP only): computes the
+ * same value as the matching batch call and stores it big-endian into the
+ * packet's checksum field (UDP.SetChecksum header/udp.go:60-62,
+ * TCP.SetChecksum header/tcp.go:156-158, IPv4.SetChecksum
+ * header/ipv4.go:165-167, ICMPv4.SetChecksum header/icmpv4.go:46-48).
+ * `out` may be NULL. `data` is written. */
+int yu_csum_fill_uniform(uint8_t *data, uint64_t stride, uint32_t len,
+                         uint64_t n, int mode,
+                         const uint16_t *initial_arr, uint16_t initial,
+                         const uint8_t *addrs, uint16_t *out, void *stream);
+int yu_csum_fill_ragged(uint8_t *data, const uint64_t *offsets, uint64_t n,
+                        int mode, const uint16_t *initial_arr,
+                        uint16_t initial, const uint8_t *addrs, uint16_t *out,
+                        void *stream);
+
+/* ------------------------------------------------------------------ */
+/* Batched host entry point (host memory in, host memory out).         */
+/* ------------------------------------------------------------------ */
+
+/* Same contract as yu_csum_batch_uniform but every pointer is a HOST
+ * pointer (pageable or pinned). The batch is cut into slices that are
+ * staged through library-owned pinned buffers on `device` and pipelined
+ * (H2D of slice k+1 overlaps the kernel of slice k and the D2H of slice
+ * k-1). Synchronous: returns when h_out is complete. Thread-safe (one
+ * staging context per calling thread and device). */
+int yu_csum_batch_host_uniform(const uint8_t *h_data, uint64_t stride,
+                               uint32_t len, uint64_t n, int mode,
+                               const uint16_t *h_initial_arr,
+                               uint16_t initial, const uint8_t *h_addrs,
+                               uint16_t *h_out, int device);
+
+/* ------------------------------------------------------------------ */
+/* Introspection.                                                      */
+/* ------------------------------------------------------------------ */
+int yu_abi_version(void);
+const char *yu_strerror(int status);
+/* Number of HIP devices (0 when none / no driver). Never fails. */
+int yu_device_count(void);
+/* Name of the kernel variant the uniform path would launch for this shape
+ * (for profiling and tests; no device needed). Returns a static string. */
+const char *yu_uniform_variant(uint64_t stride, uint32_t len, int mode,
+                               uint64_t data_align16);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* YUCSUM_H */

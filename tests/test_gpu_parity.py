@@ -1,0 +1,278 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the C oracle, bit-exact.
+
+Small cases cover every mode × layout × alignment × edge length; the full BASELINE
+configs (2, 3, 4) are compared packet-for-packet against the multithreaded C oracle
+on the same bytes.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from yustack_amd import batch
+
+pytestmark = pytest.mark.gpu
+
+EDGE_LENS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 20, 31, 32, 33, 60, 63, 64, 65, 127, 128, 129,
+             255, 256, 257, 511, 512, 513, 1023, 1024, 1025, 1499, 1500, 1501, 1535, 1536, 2047,
+             2048, 2049, 3071, 3072, 4095, 4096, 4097, 8999, 9000, 9001]
+
+
+def _to(dev, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _rand(rng, n, kind="rand"):
+    if kind == "zero":
+        return np.zeros(n, np.uint8)
+    if kind == "ff":
+        return np.full(n, 255, np.uint8)
+    return rng.integers(0, 256, size=n, dtype=np.uint8)
+
+
+def _uniform_case(dev, oracle_c, rng, length, stride, n, mode, base_off=0, kind="rand",
+                  use_addrs=False, use_init_arr=False, initial=0):
+    total = base_off + (n - 1) * stride + length + 64
+    host = _rand(rng, total, kind)
+    if mode in (O.MODE_TCP, O.MODE_VERIFY_TCP) and length >= 20:
+        for p in range(n):  # DataOffset in [20, min(60, len)], a multiple of 4
+            doff = 4 * int(rng.integers(5, min(60, length) // 4 + 1))
+            host[base_off + p * stride + 12] = (doff // 4) << 4
+    if mode in (O.MODE_IPV4, O.MODE_VERIFY_IPV4) and length >= 1:
+        for p in range(n):
+            ihl = int(rng.integers(0, 16))
+            host[base_off + p * stride] = 0x40 | ihl if ihl * 4 <= length else 0x40 | (length // 4)
+    addrs = _rand(rng, 8 * n) if use_addrs else None
+    init = rng.integers(0, 65536, size=n, dtype=np.uint16) if use_init_arr else None
+    d = _to(dev, host)
+    view = d[base_off:]
+    got = batch.checksum_uniform(view, stride, length, n, mode, initial=initial,
+                                 initial_arr=None if init is None else _to(dev, init),
+                                 addrs=None if addrs is None else _to(dev, addrs)).cpu().numpy()
+    want = oracle_c.batch(host[base_off:], mode, stride=stride, length=length, n=n,
+                          initial_arr=init, initial=initial, addrs=addrs)
+    return got, want
+
+
+@pytest.mark.parametrize("length", EDGE_LENS)
+def test_raw_uniform_edge_lengths(dev, oracle_c, length):
+    rng = np.random.default_rng(length)
+    for base_off in (0, 1, 2, 3, 5, 8, 13):
+        for stride in {length, length + 1, length + 3, max(length, 1) * 2 + 7}:
+            for kind in ("rand", "zero", "ff"):
+                got, want = _uniform_case(dev, oracle_c, rng, length, stride, 37, O.MODE_RAW,
+                                          base_off=base_off, kind=kind, use_init_arr=(kind == "rand"),
+                                          initial=0xFFFF if kind == "ff" else 0)
+                assert np.array_equal(got, want), (length, stride, base_off, kind)
+
+
+@pytest.mark.parametrize("mode", [O.MODE_UDP, O.MODE_TCP, O.MODE_VERIFY_TCP, O.MODE_VERIFY_UDP])
+@pytest.mark.parametrize("length", [20, 21, 63, 64, 65, 1499, 1500, 1501, 4097, 9000, 65535])
+def test_transport_uniform(dev, oracle_c, mode, length):
+    rng = np.random.default_rng(1000 + length + 17 * mode)
+    n = 8 if length > 9000 else 41
+    for base_off, stride_pad, use_addrs in ((0, 0, True), (3, 5, False), (2, 1, True), (1, 0, False)):
+        got, want = _uniform_case(dev, oracle_c, rng, length, length + stride_pad, n, mode,
+                                  base_off=base_off, use_addrs=use_addrs, use_init_arr=not use_addrs)
+        assert np.array_equal(got, want), (mode, length, base_off, stride_pad)
+
+
+@pytest.mark.parametrize("mode", [O.MODE_IPV4, O.MODE_VERIFY_IPV4, O.MODE_ICMP])
+@pytest.mark.parametrize("length", [4, 20, 21, 24, 60, 61, 64, 100, 1500, 1501])
+def test_ipv4_icmp_uniform(dev, oracle_c, mode, length):
+    rng = np.random.default_rng(2000 + length + 31 * mode)
+    for base_off in (0, 1, 2, 7):
+        got, want = _uniform_case(dev, oracle_c, rng, length, length + base_off, 53, mode, base_off=base_off)
+        assert np.array_equal(got, want), (mode, length, base_off)
+
+
+def _ragged(rng, lens, base_off=0, kind="rand"):
+    offs = np.zeros(len(lens) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    offs += base_off
+    return _rand(rng, int(offs[-1]) + 32, kind), offs
+
+
+@pytest.mark.parametrize("mode", list(range(8)))
+def test_ragged_all_modes(dev, oracle_c, mode):
+    rng = np.random.default_rng(3000 + mode)
+    lo = {O.MODE_UDP: 8, O.MODE_TCP: 60, O.MODE_VERIFY_TCP: 60, O.MODE_ICMP: 4,
+          O.MODE_IPV4: 60, O.MODE_VERIFY_IPV4: 60}.get(mode, 0)
+    lens = rng.integers(lo, 9001, size=600)
+    lens[:len(EDGE_LENS)] = np.maximum(np.array(EDGE_LENS), lo)
+    blob, offs = _ragged(rng, lens, base_off=3)
+    n = len(lens)
+    for p in range(n):
+        s = int(offs[p])
+        if mode in (O.MODE_TCP, O.MODE_VERIFY_TCP):
+            blob[s + 12] = int(rng.integers(5, 16)) << 4
+        if mode in (O.MODE_IPV4, O.MODE_VERIFY_IPV4):
+            blob[s] = 0x40 | int(rng.integers(0, 16))
+    addrs = _rand(rng, 8 * n)
+    init = rng.integers(0, 65536, size=n, dtype=np.uint16)
+    for use_addrs in (False, True):
+        got = batch.checksum_ragged(_to(dev, blob), _to(dev, offs.view(np.int64)), mode,
+                                    initial_arr=None if use_addrs else _to(dev, init),
+                                    addrs=_to(dev, addrs) if use_addrs else None).cpu().numpy()
+        want = oracle_c.batch(blob, mode, offsets=offs, initial_arr=None if use_addrs else init,
+                              addrs=addrs if use_addrs else None)
+        assert np.array_equal(got, want), (mode, use_addrs, np.nonzero(got != want)[0][:10])
+
+
+def test_ragged_zero_ff_and_empty(dev, oracle_c):
+    rng = np.random.default_rng(5)
+    lens = np.array([0, 0, 1, 0, 2, 3, 0, 5, 17, 0] + list(rng.integers(0, 300, size=300)))
+    for kind in ("zero", "ff", "rand"):
+        for base_off in (0, 1, 2, 3):
+            blob, offs = _ragged(rng, lens, base_off=base_off, kind=kind)
+            for initial in (0, 0xFFFF, 1234):
+                got = batch.checksum_ragged(_to(dev, blob), _to(dev, offs.view(np.int64)), "raw",
+                                            initial=initial).cpu().numpy()
+                want = oracle_c.batch(blob, O.MODE_RAW, offsets=offs, initial=initial)
+                assert np.array_equal(got, want), (kind, base_off, initial)
+    # the 0x0000-vs-0xFFFF representation: all-zero bytes with initial 0 must give 0
+    blob, offs = _ragged(rng, lens, kind="zero")
+    got = batch.checksum_ragged(_to(dev, blob), _to(dev, offs.view(np.int64)), "raw").cpu().numpy()
+    assert (got == 0).all()
+
+
+def test_raw_uint32_wrap(dev, oracle_c):
+    """Buffers > 131072 B wrap the reference's uint32 accumulator (checksum.go:5,14)."""
+    rng = np.random.default_rng(9)
+    for length in (131072, 131073, 131074, 200001, 1 << 20):
+        for kind in ("ff", "rand"):
+            for initial in (0, 0xFFFF):
+                got, want = _uniform_case(dev, oracle_c, rng, length, length + 1, 3, O.MODE_RAW,
+                                          base_off=1, kind=kind, initial=initial)
+                assert np.array_equal(got, want), (length, kind, initial)
+    host = np.full(131074, 255, np.uint8)
+    got = batch.checksum_uniform(_to(dev, host), 131074, 131074, 1, "raw", initial=0xFFFF).cpu().numpy()
+    assert got[0] == 65534  # the reference's wrapped value (exact sum would give 65535)
+
+
+@pytest.mark.parametrize("mode", [O.MODE_UDP, O.MODE_TCP, O.MODE_IPV4, O.MODE_ICMP])
+def test_fill_in_place(dev, oracle_c, mode):
+    """fill=True writes the TX field (SetChecksum); re-verifying gives 0/0xFFFF."""
+    rng = np.random.default_rng(77 + mode)
+    n, L = 333, 1500
+    host = _rand(rng, n * L)
+    pk = host.reshape(n, L)
+    if mode == O.MODE_TCP:
+        pk[:, 12] = 0x50
+    if mode == O.MODE_IPV4:
+        pk[:, 0] = 0x45
+    addrs = _rand(rng, 8 * n)
+    d = _to(dev, host)
+    a = _to(dev, addrs)
+    out = batch.checksum_uniform(d, L, L, n, mode, addrs=a if mode in (1, 2) else None, fill=True)
+    want = oracle_c.batch(host, mode, stride=L, length=L, n=n, addrs=addrs if mode in (1, 2) else None)
+    assert np.array_equal(out.cpu().numpy(), want)
+    filled = d.cpu().numpy().reshape(n, L)
+    f = {O.MODE_UDP: 6, O.MODE_TCP: 16, O.MODE_IPV4: 10, O.MODE_ICMP: 2}[mode]
+    assert np.array_equal((filled[:, f].astype(np.uint16) << 8) | filled[:, f + 1], want)
+    if mode in (O.MODE_UDP, O.MODE_TCP):
+        vmode = O.MODE_VERIFY_UDP if mode == O.MODE_UDP else O.MODE_VERIFY_TCP
+        v = batch.checksum_uniform(d, L, L, n, vmode, addrs=a)
+        assert bool(batch.verified(v).all())
+    if mode == O.MODE_IPV4:
+        v = batch.checksum_uniform(d, L, L, n, O.MODE_VERIFY_IPV4)
+        assert bool(batch.verified(v).all())
+
+
+def test_reference_harness_packets_verify(dev):
+    """Packets built exactly like the reference test harnesses
+    (context.go:164-209, udp_test.go:105-144) pass the batched checker modes."""
+    from yustack_amd import packets
+    rng = np.random.default_rng(11)
+    pk = [packets.tcp_test_packet(bytes(rng.integers(0, 256, int(rng.integers(0, 1460)), dtype=np.uint8)),
+                                  4096, 1234, 790, 1000, 0x18, 30000) for _ in range(64)]
+    offs = np.zeros(len(pk) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(p) for p in pk])
+    blob = np.frombuffer(b"".join(bytes(p) for p in pk), dtype=np.uint8)
+    v = batch.checksum_ragged(_to(dev, blob), _to(dev, offs), "verify_ipv4")
+    assert bool(batch.verified(v).all())
+    segs = [bytes(p[20:]) for p in pk]
+    soffs = np.zeros(len(segs) + 1, dtype=np.int64)
+    soffs[1:] = np.cumsum([len(s) for s in segs])
+    sblob = np.frombuffer(b"".join(segs), dtype=np.uint8)
+    addrs = np.frombuffer(b"".join(bytes(p[12:20]) for p in pk), dtype=np.uint8)
+    v = batch.checksum_ragged(_to(dev, sblob), _to(dev, soffs), "verify_tcp", addrs=_to(dev, addrs))
+    assert bool(batch.verified(v).all())
+    # one corrupted byte must fail verification
+    bad = sblob.copy()
+    bad[soffs[3] + 25] ^= 0x10
+    v = batch.checksum_ragged(_to(dev, bad), _to(dev, soffs), "verify_tcp", addrs=_to(dev, addrs))
+    ok = batch.verified(v).cpu().numpy()
+    assert not ok[3] and ok[np.arange(len(segs)) != 3].all()
+
+
+def test_host_uniform_path(dev, oracle_c):
+    rng = np.random.default_rng(21)
+    for n, L, stride in ((100000, 1500, 1500), (70000, 64, 64), (1000, 9000, 9003), (3, 5, 7)):
+        host = _rand(rng, (n - 1) * stride + L)
+        host[12::stride] = 0x50 if L >= 20 else host[12::stride]
+        addrs = _rand(rng, 8 * n)
+        mode = O.MODE_TCP if L >= 20 else O.MODE_RAW
+        got = batch.checksum_host_uniform(host, stride, L, n, mode, addrs=addrs)
+        want = oracle_c.batch(host, mode, stride=stride, length=L, n=n, addrs=addrs, threads=8)
+        assert np.array_equal(got, want), (n, L, stride)
+    # pinned input goes straight to the copy engine
+    pinned = torch.from_numpy(_rand(rng, 4096 * 1500)).pin_memory()
+    got = batch.checksum_host_uniform(pinned, 1500, 1500, 4096, "raw")
+    want = oracle_c.batch(pinned.numpy(), O.MODE_RAW, stride=1500, length=1500, n=4096)
+    assert np.array_equal(got, want)
+
+
+def test_errors_are_loud(dev):
+    from yustack_amd._lib import YuError
+    d = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    with pytest.raises(YuError):
+        batch.checksum_uniform(d, 16, 70000, 1, "tcp")  # > 65535 in a transport mode
+    with pytest.raises(YuError):
+        batch.checksum_uniform(d, 16, 4, 1, "udp")  # shorter than the UDP header
+    with pytest.raises(ValueError):
+        batch.checksum_uniform(d, 4096, 16, 2, "raw")  # runs past the buffer
+    with pytest.raises(TypeError):
+        batch.checksum_uniform(d.cpu(), 16, 16, 1, "raw")
+
+
+# ------------------------------------------------------------------ full size
+def _full_uniform(dev, oracle_c, n, L, mode, use_addrs, use_init):
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + L)
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+    if mode == O.MODE_TCP:
+        d.view(n, L)[:, 12] = 0x50
+        d.view(n, L)[:, 16:18] = 0
+    a = torch.randint(0, 256, (8 * n,), dtype=torch.uint8, device=dev, generator=g) if use_addrs else None
+    i = torch.randint(0, 65536, (n,), dtype=torch.int32, device=dev, generator=g).to(torch.uint16) if use_init else None
+    got = batch.checksum_uniform(d, L, L, n, mode, addrs=a, initial_arr=i).cpu().numpy()
+    want = oracle_c.batch(d.cpu().numpy(), mode, stride=L, length=L, n=n,
+                          addrs=None if a is None else a.cpu().numpy(),
+                          initial_arr=None if i is None else i.cpu().numpy(), threads=16)
+    return got, want
+
+
+def test_full_config2_raw_64B(dev, oracle_c):
+    got, want = _full_uniform(dev, oracle_c, 1 << 20, 64, O.MODE_RAW, False, True)
+    assert np.array_equal(got, want)
+
+
+def test_full_config3_tcp_1500B(dev, oracle_c):
+    got, want = _full_uniform(dev, oracle_c, 1 << 20, 1500, O.MODE_TCP, True, False)
+    assert np.array_equal(got, want)
+
+
+def test_full_config4_ragged(dev, oracle_c):
+    n = 1 << 20
+    rng = np.random.default_rng(4)
+    lens = rng.integers(64, 9001, size=n)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    g = torch.Generator(device=dev)
+    g.manual_seed(4)
+    d = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device=dev, generator=g)
+    init = rng.integers(0, 65536, size=n, dtype=np.uint16)
+    got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), "raw", initial_arr=_to(dev, init)).cpu().numpy()
+    want = oracle_c.batch(d.cpu().numpy(), O.MODE_RAW, offsets=offs, initial_arr=init, threads=16)
+    assert np.array_equal(got, want)

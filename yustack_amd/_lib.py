@@ -1,0 +1,86 @@
+"""Loader for the in-tree C-ABI library ``yustack_amd/libyucsum.so`` (include/yucsum.h).
+
+There is no fallback: if the library is missing or cannot be loaded, importing
+anything that needs it raises, and the batched (GPU) entry points return a negative
+status that :func:`check` turns into an exception when no HIP device is usable.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libyucsum.so")
+
+# Exported symbols declared in include/yucsum.h (checked by tests/test_abi.py).
+EXPORTS = (
+    "yu_checksum", "yu_checksum_combine", "yu_pseudo_header_checksum",
+    "yu_csum_batch_uniform", "yu_csum_batch_ragged",
+    "yu_csum_fill_uniform", "yu_csum_fill_ragged",
+    "yu_csum_batch_host_uniform",
+    "yu_abi_version", "yu_strerror", "yu_device_count", "yu_uniform_variant",
+)
+
+YU_OK, YU_EINVAL, YU_ENODEV, YU_ENOMEM, YU_EHIP_BASE = 0, -22, -19, -12, -1000
+
+
+class YuError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what} failed: status {status} ({strerror(status)})")
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not built — run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C yustack_amd/csrc`")
+    L = ctypes.CDLL(LIB_PATH)
+    c = ctypes
+    vp, u8, u16, u32, u64, sz, i32 = (c.c_void_p, c.c_uint8, c.c_uint16, c.c_uint32,
+                                      c.c_uint64, c.c_size_t, c.c_int)
+    L.yu_checksum.restype = u16
+    L.yu_checksum.argtypes = [vp, sz, u16]
+    L.yu_checksum_combine.restype = u16
+    L.yu_checksum_combine.argtypes = [u16, u16]
+    L.yu_pseudo_header_checksum.restype = u16
+    L.yu_pseudo_header_checksum.argtypes = [u32, vp, sz, vp, sz]
+    for name in ("yu_csum_batch_uniform", "yu_csum_fill_uniform"):
+        f = getattr(L, name)
+        f.restype = i32
+        f.argtypes = [vp, u64, u32, u64, i32, vp, u16, vp, vp, vp]
+    for name in ("yu_csum_batch_ragged", "yu_csum_fill_ragged"):
+        f = getattr(L, name)
+        f.restype = i32
+        f.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, vp]
+    L.yu_csum_batch_host_uniform.restype = i32
+    L.yu_csum_batch_host_uniform.argtypes = [vp, u64, u32, u64, i32, vp, u16, vp, vp, i32]
+    L.yu_abi_version.restype = i32
+    L.yu_abi_version.argtypes = []
+    L.yu_strerror.restype = c.c_char_p
+    L.yu_strerror.argtypes = [i32]
+    L.yu_device_count.restype = i32
+    L.yu_device_count.argtypes = []
+    L.yu_uniform_variant.restype = c.c_char_p
+    L.yu_uniform_variant.argtypes = [u64, u32, i32, u64]
+    del u8
+    _lib = L
+    return L
+
+
+def strerror(status: int) -> str:
+    try:
+        return lib().yu_strerror(status).decode()
+    except Exception:  # pragma: no cover - only when the library itself is unusable
+        return "unknown"
+
+
+def check(status: int, what: str) -> None:
+    if status != YU_OK:
+        raise YuError(status, what)

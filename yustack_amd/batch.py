@@ -1,0 +1,181 @@
+"""Batched Internet checksum on MI355X — the hot path.
+
+Thin Python front end over the C ABI's batched entry points
+(``yu_csum_batch_uniform`` / ``yu_csum_batch_ragged`` / ``yu_csum_fill_*`` /
+``yu_csum_batch_host_uniform``, include/yucsum.h). PyTorch is used only for device
+memory and streams: the arithmetic happens in the hand-written gfx950 kernels of
+``csrc/yucsum_kernels.hip``. There is no CPU fallback — without a HIP device every
+entry point raises :class:`yustack_amd._lib.YuError`.
+
+Modes (each reproduces one reference composition, see include/yucsum.h):
+
+=============  =========================================================================
+RAW            ``Checksum(pkt, initial)``                     checksum/checksum.go:4-18
+UDP            field value of sendUDP                          transport/udp/endpoint.go:164-187
+TCP            field value of sendTCP                          transport/tcp/connect.go:556-586
+IPV4           field value of ipv4 WritePacket                 network/ipv4/ipv4.go:80-97
+ICMP           field value of sendICMPv4                       network/ipv4/icmp.go:36-45
+VERIFY_IPV4    checker.IPv4 sum (valid iff 0 or 0xFFFF)        checker/checker.go:25-40
+VERIFY_TCP     checker.TCP sum                                 checker/checker.go:71-99
+VERIFY_UDP     the checker.TCP formula for UDP
+=============  =========================================================================
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._lib import check, lib
+
+RAW, UDP, TCP, IPV4, ICMP, VERIFY_IPV4, VERIFY_TCP, VERIFY_UDP = range(8)
+MODES = {"raw": RAW, "udp": UDP, "tcp": TCP, "ipv4": IPV4, "icmp": ICMP,
+         "verify_ipv4": VERIFY_IPV4, "verify_tcp": VERIFY_TCP, "verify_udp": VERIFY_UDP}
+TX_MODES = (UDP, TCP, IPV4, ICMP)
+MAX_TRANSPORT_LEN = 65535
+
+
+def _mode(m) -> int:
+    m = MODES[m] if isinstance(m, str) else int(m)
+    if not 0 <= m < 8:
+        raise ValueError(f"bad mode {m}")
+    return m
+
+
+def _dev_u8(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor")
+    if t.dtype != torch.uint8 or not t.is_contiguous():
+        raise TypeError(f"{name} must be a contiguous uint8 tensor")
+    return t
+
+
+def _opt(t, dtype, numel, device, name):
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.device != device:
+        raise TypeError(f"{name} must be a CUDA tensor on {device}")
+    if t.dtype != dtype or not t.is_contiguous() or t.numel() < numel:
+        raise TypeError(f"{name} must be a contiguous {dtype} tensor with >= {numel} elements")
+    return t
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(device, stream):
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return s.cuda_stream
+
+
+def checksum_uniform(data: torch.Tensor, stride: int, length: int, n: int, mode="raw", *,
+                     initial: int = 0, initial_arr: torch.Tensor | None = None,
+                     addrs: torch.Tensor | None = None, out: torch.Tensor | None = None,
+                     stream: torch.cuda.Stream | None = None, fill: bool = False) -> torch.Tensor:
+    """Per-packet sums of a uniform-stride device batch: packet i is
+    ``data[i*stride : i*stride+length]``. Returns a uint16 tensor of n results
+    (allocated unless ``out`` is given). ``fill=True`` additionally stores each TX
+    result big-endian into the packet's checksum field (in place)."""
+    m = _mode(mode)
+    _dev_u8(data, "data")
+    if n < 0 or stride < 0 or not 0 <= length < 2 ** 32:
+        raise ValueError("bad geometry")
+    if n and (n - 1) * stride + length > data.numel():
+        raise ValueError(f"batch needs {(n - 1) * stride + length} bytes, data has {data.numel()}")
+    dev = data.device
+    initial_arr = _opt(initial_arr, torch.uint16, n, dev, "initial_arr")
+    addrs = _opt(addrs, torch.uint8, 8 * n, dev, "addrs")
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.uint16, device=dev)[:n]
+    else:
+        _opt(out, torch.uint16, n, dev, "out")
+    with torch.cuda.device(dev):
+        f = lib().yu_csum_fill_uniform if fill else lib().yu_csum_batch_uniform
+        rc = f(data.data_ptr(), stride, length, n, m, _ptr(initial_arr), initial & 0xFFFF,
+               _ptr(addrs), out.data_ptr() if n else None, _stream(dev, stream))
+    check(rc, "yu_csum_fill_uniform" if fill else "yu_csum_batch_uniform")
+    return out
+
+
+def checksum_ragged(data: torch.Tensor, offsets: torch.Tensor, mode="raw", *, initial: int = 0,
+                    initial_arr: torch.Tensor | None = None, addrs: torch.Tensor | None = None,
+                    out: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None,
+                    fill: bool = False, validate: bool = True) -> torch.Tensor:
+    """Per-packet sums of a ragged device batch: packet i is
+    ``data[offsets[i] : offsets[i+1]]`` (offsets: n+1 non-decreasing int64/uint64).
+    ``validate`` checks the offsets against ``data`` on the device before launching
+    (one small synchronisation); pass False only for offsets validated earlier."""
+    m = _mode(mode)
+    _dev_u8(data, "data")
+    if not isinstance(offsets, torch.Tensor) or not offsets.is_cuda or offsets.device != data.device:
+        raise TypeError("offsets must be a CUDA tensor on data's device")
+    if offsets.dtype not in (torch.int64, torch.uint64) or not offsets.is_contiguous() or offsets.dim() != 1:
+        raise TypeError("offsets must be a contiguous 1-D int64/uint64 tensor")
+    n = offsets.numel() - 1
+    if n < 0:
+        raise ValueError("offsets must hold n+1 entries")
+    if validate and n > 0:
+        o = offsets.view(torch.int64)
+        ok = bool(((o[1:] >= o[:-1]).all() & (o[0] >= 0) & (o[-1] <= data.numel())).item())
+        if not ok:
+            raise ValueError("offsets are not non-decreasing within data")
+        if m != RAW and bool(((o[1:] - o[:-1]) > MAX_TRANSPORT_LEN).any().item()):
+            raise ValueError("transport/IPv4/ICMP packets must be <= 65535 bytes")
+    dev = data.device
+    initial_arr = _opt(initial_arr, torch.uint16, n, dev, "initial_arr")
+    addrs = _opt(addrs, torch.uint8, 8 * n, dev, "addrs")
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.uint16, device=dev)[:n]
+    else:
+        _opt(out, torch.uint16, n, dev, "out")
+    with torch.cuda.device(dev):
+        f = lib().yu_csum_fill_ragged if fill else lib().yu_csum_batch_ragged
+        rc = f(data.data_ptr(), offsets.data_ptr(), n, m, _ptr(initial_arr), initial & 0xFFFF,
+               _ptr(addrs), out.data_ptr() if n else None, _stream(dev, stream))
+    check(rc, "yu_csum_fill_ragged" if fill else "yu_csum_batch_ragged")
+    return out
+
+
+def checksum_host_uniform(data: np.ndarray, stride: int, length: int, n: int, mode="raw", *,
+                          initial: int = 0, initial_arr: np.ndarray | None = None,
+                          addrs: np.ndarray | None = None, out: np.ndarray | None = None,
+                          device: int = 0) -> np.ndarray:
+    """Host-memory batch in, host-memory results out (pinned staging + pipelined
+    H2D/kernel/D2H inside the library). ``data`` may be a numpy array or a pinned
+    torch CPU tensor (then the copy engine reads it directly)."""
+    m = _mode(mode)
+    if isinstance(data, torch.Tensor):
+        if data.is_cuda or data.dtype != torch.uint8 or not data.is_contiguous():
+            raise TypeError("data must be a contiguous uint8 CPU tensor")
+        dptr, dlen = data.data_ptr(), data.numel()
+    else:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        dptr, dlen = data.ctypes.data, data.size
+    if n and (n - 1) * stride + length > dlen:
+        raise ValueError("data too small for the batch geometry")
+    ia = None if initial_arr is None else np.ascontiguousarray(initial_arr, dtype=np.uint16)
+    ad = None if addrs is None else np.ascontiguousarray(addrs, dtype=np.uint8)
+    if ia is not None and ia.size < n or ad is not None and ad.size < 8 * n:
+        raise ValueError("side arrays too small")
+    if out is None:
+        out = np.empty(n, dtype=np.uint16)
+    if isinstance(out, torch.Tensor):
+        optr = out.data_ptr()
+    else:
+        optr = out.ctypes.data
+    rc = lib().yu_csum_batch_host_uniform(dptr, stride, length, n, m,
+                                          None if ia is None else ia.ctypes.data, initial & 0xFFFF,
+                                          None if ad is None else ad.ctypes.data, optr, device)
+    check(rc, "yu_csum_batch_host_uniform")
+    return out
+
+
+def verified(sums: torch.Tensor) -> torch.Tensor:
+    """checker semantics: a VERIFY_* sum is valid iff it is 0x0000 or 0xFFFF."""
+    s = sums.view(torch.int16)
+    return (s == 0) | (s == -1)
+
+
+def variant(stride: int, length: int, mode="raw", align16: int = 0) -> str:
+    """Name of the kernel the uniform path launches for this geometry."""
+    return lib().yu_uniform_variant(stride, length, _mode(mode), align16).decode()
