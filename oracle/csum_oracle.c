@@ -143,9 +143,11 @@ uint16_t or_packet(int mode, const uint8_t *pkt, uint64_t len,
     }
     case OR_MODE_IPV4: {
       /* network/ipv4/ipv4.go:80-97 */
-      size_t hl = (size_t)(pkt[0] & 0xf) * 4;
-      memcpy(hdr, pkt, hl);
-      if (hl >= 12) hdr[10] = hdr[11] = 0; /* Encode: Checksum zero value */
+      /* the packet as Encode left it: same bytes, checksum field 0; the
+       * header length is read from byte 0 of that packet */
+      size_t cp = len < sizeof(hdr) ? (size_t)len : sizeof(hdr);
+      memcpy(hdr, pkt, cp);
+      if (cp >= 12) hdr[10] = hdr[11] = 0; /* Encode: Checksum zero value */
       return (uint16_t)~or_ipv4_calculate_checksum(hdr);
     }
     case OR_MODE_ICMP: {

@@ -140,9 +140,8 @@ def packet(mode: int, pkt: bytes, initial_arr=None, initial: int = 0, addrs=None
         xsum = checksum(data, xsum)
         return ~tcp_calculate_checksum(bytes(hdr), xsum, length) & 0xFFFF
     if mode == MODE_IPV4:  # network/ipv4/ipv4.go:80-97
-        hl = (pkt[0] & 0xF) * 4
-        hdr = bytearray(pkt[:hl])
-        if hl >= 12:
+        hdr = bytearray(pkt[:64])  # the packet as Encode left it (field 0)
+        if len(hdr) >= 12:
             hdr[10:12] = b"\0\0"
         return ~ipv4_calculate_checksum(bytes(hdr)) & 0xFFFF
     if mode == MODE_ICMP:  # network/ipv4/icmp.go:36-45

@@ -225,13 +225,13 @@ def test_host_uniform_path(dev, oracle_c):
 
 def test_errors_are_loud(dev):
     from yustack_amd._lib import YuError
-    d = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    d = torch.zeros(1 << 17, dtype=torch.uint8, device=dev)
     with pytest.raises(YuError):
         batch.checksum_uniform(d, 16, 70000, 1, "tcp")  # > 65535 in a transport mode
     with pytest.raises(YuError):
         batch.checksum_uniform(d, 16, 4, 1, "udp")  # shorter than the UDP header
     with pytest.raises(ValueError):
-        batch.checksum_uniform(d, 4096, 16, 2, "raw")  # runs past the buffer
+        batch.checksum_uniform(d, 1 << 17, 16, 2, "raw")  # runs past the buffer
     with pytest.raises(TypeError):
         batch.checksum_uniform(d.cpu(), 16, 16, 1, "raw")
 

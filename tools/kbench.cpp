@@ -1,0 +1,94 @@
+// kbench.cpp — measurement tool (not product): times the C-ABI batch entry
+// points on BASELINE configs 2/3/4 with HIP events, without Python/torch in
+// the loop, for quick kernel A/B work and rocprofv3 runs.
+//
+// build: hipcc -O2 -I include tools/kbench.cpp -o tools/kbench -L yustack_amd -lyucsum -Wl,-rpath,'$ORIGIN/../yustack_amd'
+// run:   tools/kbench [config...]   (default 2 3 4)
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <random>
+#include <vector>
+
+#include "yucsum.h"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+  fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1);} } while (0)
+
+__global__ void fill(uint8_t *p, uint64_t n, uint32_t seed) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n / 4; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t x = ((uint32_t)i ^ seed) * 2654435761u;
+    x ^= x >> 15;
+    x *= 0x2c1b3c6du;
+    x ^= x >> 12;
+    ((uint32_t *)p)[i] = x;
+  }
+}
+
+int main(int argc, char **argv) {
+  std::vector<int> cfgs;
+  for (int i = 1; i < argc; ++i) cfgs.push_back(atoi(argv[i]));
+  if (cfgs.empty()) cfgs = {2, 3, 4};
+  const uint64_t n = 1ull << 20;
+  const int reps = 30, rounds = 3;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  uint16_t *out, *init;
+  uint8_t *addrs;
+  CK(hipMalloc(&out, n * 2));
+  CK(hipMalloc(&init, n * 2));
+  CK(hipMalloc(&addrs, n * 8));
+  fill<<<1024, 256>>>((uint8_t *)init, n * 2, 11);
+  fill<<<1024, 256>>>(addrs, n * 8, 12);
+  for (int cfg : cfgs) {
+    uint64_t bytes = 0, alg = 0;
+    uint32_t L = 0;
+    int mode = 0;
+    uint64_t *d_off = nullptr;
+    if (cfg == 2) { L = 64; mode = YU_MODE_RAW; bytes = n * L; alg = bytes + 4 * n; }
+    if (cfg == 3) { L = 1500; mode = YU_MODE_TCP; bytes = n * L; alg = bytes + 10 * n; }
+    if (cfg == 4) {
+      std::mt19937_64 rng(4);
+      std::uniform_int_distribution<int> d(64, 9000);
+      std::vector<uint64_t> off(n + 1, 0);
+      for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + d(rng);
+      bytes = off[n];
+      alg = bytes + 8 * (n + 1) + 4 * n;
+      CK(hipMalloc(&d_off, (n + 1) * 8));
+      CK(hipMemcpy(d_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+    }
+    int R = (int)((2ull << 30) / bytes + 1);
+    std::vector<uint8_t *> bufs(R);
+    for (int r = 0; r < R; ++r) {
+      CK(hipMalloc(&bufs[r], bytes + 64));
+      fill<<<4096, 256>>>(bufs[r], bytes + 64, 100 + r);
+    }
+    CK(hipDeviceSynchronize());
+    auto launch = [&](int k) {
+      int rc = d_off ? yu_csum_batch_ragged(bufs[k % R], d_off, n, mode, init, 0, nullptr, out, nullptr)
+                     : yu_csum_batch_uniform(bufs[k % R], L, L, n, mode, cfg == 2 ? init : nullptr, 0,
+                                             cfg == 3 ? addrs : nullptr, out, nullptr);
+      if (rc) { fprintf(stderr, "rc %d\n", rc); exit(1); }
+    };
+    for (int r = 0; r < rounds; ++r) {
+      for (int k = 0; k < 3; ++k) launch(k);
+      CK(hipEventRecord(e0));
+      for (int k = 0; k < reps; ++k) launch(k);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      double s = ms / 1e3 / reps;
+      printf("config%d round %d: %8.1f us/launch  %7.1f GB/s alg  (%.3f of 8 TB/s)  %s\n", cfg, r, s * 1e6,
+             alg / s / 1e9, alg / s / 8e12,
+             d_off ? "k_loop<4>" : yu_uniform_variant(L, L, mode, (uintptr_t)bufs[0] & 15));
+    }
+    for (auto b : bufs) CK(hipFree(b));
+    if (d_off) CK(hipFree(d_off));
+  }
+  return 0;
+}

@@ -11,33 +11,44 @@
 //                           network/ipv4/ipv4.go:80-97, network/ipv4/icmp.go:36-45,
 //                           checker/checker.go:25-40,71-99
 //
-// Arithmetic. The reference accumulates big-endian 16-bit words in a uint32
-// that wraps mod 2^32 and folds once. Addition mod 2^32 is order-free, so any
-// split of the packet across lanes, summed in uint32, reproduces the
-// reference accumulator bit for bit (including the wrap for RAW buffers
-// > 131072 B). Per 32-bit dword loaded little-endian from HBM:
-//   v_perm_b32  swaps the bytes of each 16-bit half when the packet starts at
-//               an even address (so each half becomes the big-endian word the
-//               reference adds; for odd-start packets the little-endian halves
-//               already carry the right weights and the perm is the identity);
-//   v_sad_u16   adds both 16-bit halves into the uint32 accumulator.
-// Two VALU ops per 4 bytes: the kernel stays far below the VALU ceiling and is
-// bound by HBM.
+// Arithmetic. The reference adds big-endian 16-bit words into a uint32 that
+// wraps mod 2^32 and folds once (ChecksumCombine). Two exact formulations:
 //
-// Layout. Loads are 16-byte (global_load_dwordx4) at 16-byte aligned
-// addresses. A packet [s, e) is covered by the aligned chunks from
-// floor16(s). Dwords are included iff they overlap [s, e) (one unsigned
-// compare each); the few bytes a dword-granular include gets wrong — the
-// head bytes before an unaligned s, the tail bytes after an unaligned e, and
-// in TX modes the checksum field that Encode() zeroes — are subtracted on a
-// rare, divergent correction path that only the lanes holding them enter.
+//  * LE (default). Sum the little-endian 16-bit halves of every 32-bit word
+//    with v_sad_u16 — ONE VALU op per 4 bytes — into a uint32 S_LE. Swapping
+//    the bytes of a 16-bit word multiplies it by 256 modulo 65535, so the
+//    big-endian sum S_BE is congruent to swap16(fold(S_LE)) when the packet
+//    starts at an even address (to fold(S_LE) when it starts at an odd one),
+//    and S_BE is 0 exactly when S_LE is. The reference's result depends on
+//    S_BE only through that residue and zero-ness as long as its uint32 does
+//    not wrap, i.e. for buffers <= 131072 bytes: every transport/IPv4/ICMP
+//    packet and every RAW packet up to that size.
+//  * BE (RAW packets that may exceed 131072 bytes). v_perm_b32 turns each
+//    16-bit half into the big-endian word first; the uint32 sum then equals
+//    the reference's accumulator bit for bit, wrap included (addition mod
+//    2^32 is order-free).
+//
+// Layout. A packet [s, e) is read through 16-byte loads (buffer_load_dwordx4)
+// from a window that starts at floor4(s): every chunk but the last lies
+// inside the packet and is summed unmasked; the last chunk's dwords are kept
+// iff they start before e. The few bytes this gets wrong — up to 3 bytes
+// before an unaligned s, up to 3 after an unaligned e, and in TX modes the
+// two checksum-field bytes that Encode() zeroes — sit in at most four known
+// dwords; the group leader loads those dwords once more (same cache lines)
+// and subtracts their masked bytes.
+//
+// Loads go through buffer descriptors based at wave-uniform addresses: a lane
+// that must not load passes an out-of-range offset and gets zeros without a
+// memory access, so no load sits in an exec-masked block and the compiler's
+// vmcnt bookkeeping stays exact. That lets the kernels keep the next step's
+// loads in flight while the current step is summed (software pipelining).
 //
 // Work mapping (wave64-first, not a warp tiling):
 //   k_small<G, U>: uniform stride, packet span <= G*U*16 bytes. A wave holds
 //     64/G packets per step; each group of G lanes loads its packet window in
 //     U dwordx4 loads per lane (1 KiB per wave-instruction), reduces with
-//     log2(G) cross-lane adds and its leader stores the uint16 result.
-//   k_loop<U>: one wave per packet, looping over 64*U*16-byte windows. Used for
+//     log2(G) DPP adds and its last lane finishes the packet.
+//   k_loop<U, BE>: one wave per packet, looping over 64*U*16-byte windows, for
 //     ragged (tun-style, any alignment) batches and uniform packets > 4 KiB.
 //   Both are persistent grid-stride kernels sized to the CU count.
 #include <hip/hip_runtime.h>
@@ -54,6 +65,7 @@ namespace {
 
 constexpr uint32_t kSelSwap = 0x02030001u;  // bytes [1,0,3,2]: BE 16-bit halves
 constexpr uint32_t kSelIdent = 0x03020100u; // bytes [0,1,2,3]
+constexpr uint32_t kLEMax = 131072u;        // longest packet the LE sum covers
 
 struct BatchArgs {
   const uint8_t *data;
@@ -64,8 +76,10 @@ struct BatchArgs {
   uint8_t *fill;  // non-null: write the field into the packet (== data)
   uint64_t stride;
   uint64_t n;
+  uint64_t end;   // one past the batch's last byte (uniform); ragged: 0
   uint32_t len;
   uint32_t initial;
+  uint32_t uf;    // k_small: steps u < uf hold only full chunks
   int mode;
 };
 
@@ -112,130 +126,175 @@ __device__ __forceinline__ uint32_t fold32(uint32_t v) {
   return (w + (w >> 16)) & 0xFFFFu;
 }
 
+__device__ __forceinline__ uint32_t sad(uint32_t x, uint32_t acc) {
+  return __builtin_amdgcn_sad_u16(x, 0u, acc);
+}
+
 __device__ __forceinline__ uint32_t sadperm(uint32_t x, uint32_t sel,
                                             uint32_t acc) {
   return __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(x, x, sel), 0u, acc);
 }
 
-// Bytes of the dword [d, d+4) that lie in [x0, x1) as a byte mask
-// (rare path only).
-__device__ __forceinline__ uint32_t range_mask(uint32_t d, uint32_t x0,
-                                               uint32_t x1) {
-  int64_t lo = (int64_t)x0 - (int64_t)d;
-  int64_t hi = (int64_t)x1 - (int64_t)d;
-  lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
-  hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
-  if (hi <= lo) return 0u;
-  uint64_t m = ((1ull << (8 * hi)) - 1ull) ^ ((1ull << (8 * lo)) - 1ull);
-  return (uint32_t)m;
+template <bool BE>
+__device__ __forceinline__ uint32_t add_word(uint32_t x, uint32_t sel,
+                                             uint32_t acc) {
+  return BE ? sadperm(x, sel, acc) : sad(x, acc);
 }
 
-__device__ __forceinline__ bool overlaps(uint32_t a0, uint32_t a1, uint32_t b0,
-                                         uint32_t b1) {
-  return b0 < b1 && b0 < a1 && a0 < b1;
+// Residue of the packet's big-endian word sum, from the LE sum of a packet
+// starting at an address of parity `odd` (see the header comment).
+__device__ __forceinline__ uint32_t le_to_be(uint32_t s_le, uint32_t odd) {
+  const uint32_t r = fold32(s_le);
+  return odd ? r : (((r & 0xFFu) << 8) | (r >> 8));
 }
 
-// Packet geometry in window-relative byte coordinates (window base =
-// floor16(packet start)).
-struct Geom {
-  uint32_t s;     // packet start (0..15)
-  uint32_t e;     // end of the summed bytes
-  uint32_t s4;    // floor4(s)
-  uint32_t L4;    // e - s4: dword d (rel) included iff d - s4 < L4
-  uint32_t sel;   // perm selector (parity of s)
-  uint32_t h1;    // head junk [s4, h1=s)
-  uint32_t t0, t1;  // tail junk [e, ceil4(e))
-  uint32_t f0, f1;  // TX field [f0, f1) ∩ [s, e)
-  bool junk;      // any junk range non-empty
-};
-
-__device__ __forceinline__ Geom make_geom(uint32_t s, uint32_t e, int mode) {
-  Geom g;
-  g.s = s;
-  g.e = e;
-  g.s4 = s & ~3u;
-  g.L4 = e - g.s4;
-  g.sel = (s & 1u) ? kSelIdent : kSelSwap;
-  g.h1 = s;
-  g.t0 = e;
-  g.t1 = (e & 3u) ? ((e + 3u) & ~3u) : e;
-  if (mode_is_tx(mode)) {
-    uint32_t f0 = s + mode_field(mode);
-    uint32_t f1 = f0 + 2u;
-    f0 = f0 < e ? f0 : e;
-    f1 = f1 < e ? f1 : e;
-    g.f0 = f0;
-    g.f1 = f1;
-  } else {
-    g.f0 = g.f1 = 0;
-  }
-  g.junk = (s & 3u) || (e & 3u) || (g.f0 < g.f1);
-  return g;
-}
-
-// Accumulate one 16-byte chunk at window-relative offset cr.
-__device__ __forceinline__ void sum_chunk(const uint4 &c, uint32_t cr,
-                                          const Geom &g, uint32_t &acc) {
-  const uint32_t r = cr - g.s4;
-  const uint32_t x0 = (r < g.L4) ? c.x : 0u;
-  const uint32_t x1 = (r + 4u < g.L4) ? c.y : 0u;
-  const uint32_t x2 = (r + 8u < g.L4) ? c.z : 0u;
-  const uint32_t x3 = (r + 12u < g.L4) ? c.w : 0u;
-  acc = sadperm(x0, g.sel, acc);
-  acc = sadperm(x1, g.sel, acc);
-  acc = sadperm(x2, g.sel, acc);
-  acc = sadperm(x3, g.sel, acc);
-  if (g.junk) {
-    const uint32_t ce = cr + 16u;
-    if (overlaps(cr, ce, g.s4, g.h1) || overlaps(cr, ce, g.t0, g.t1) ||
-        overlaps(cr, ce, g.f0, g.f1)) {
-      uint32_t junk = 0;
-      const uint32_t xs[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t d = cr + 4u * j;
-        const uint32_t m = range_mask(d, g.s4, g.h1) |
-                           range_mask(d, g.t0, g.t1) |
-                           range_mask(d, g.f0, g.f1);
-        junk = sadperm(xs[j] & m, g.sel, junk);
-      }
-      acc -= junk;
-    }
-  }
-}
-
-// Byte at window-relative offset s (0..15) of chunk 0.
-__device__ __forceinline__ uint32_t byte_of(const uint4 &c, uint32_t s) {
-  const uint32_t di = s >> 2;
-  const uint32_t w = di == 0 ? c.x : (di == 1 ? c.y : (di == 2 ? c.z : c.w));
-  return (w >> (8u * (s & 3u))) & 0xFFu;
-}
-
+// Sum over each aligned group of G lanes; the total lands in the group's
+// LAST lane (lane % G == G-1). DPP row shifts inside 16-lane rows, then
+// row_bcast15/31 across rows — VALU only, no LDS traffic.
 template <int G>
-__device__ __forceinline__ uint32_t group_sum(uint32_t v) {
-#pragma unroll
-  for (int o = G / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+__device__ __forceinline__ uint32_t group_total(uint32_t v) {
+  static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two");
+  if (G >= 2) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  if (G >= 4) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  if (G >= 8) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  if (G >= 16) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true); // row_shr:8
+  if (G >= 32) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); // row_bcast:15
+  if (G >= 64) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); // row_bcast:31
   return v;
 }
 
-// Per-packet epilogue: add the non-payload terms of the reference
-// composition, fold, complement, store (and optionally set the field).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Wave-uniform 64-bit value (only for values uniform by construction): puts
+// buffer bases in SGPRs so no waterfall loop is generated.
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Out-of-range offset: the load returns zeros and touches no memory.
+constexpr uint32_t kOOB = 0x80000000u;
+
+// Descriptor over [base, min(ceil4(end), base + 2 GiB)). The range check is
+// per dword (a dword reaching past num_records reads as 0), so the extent is
+// rounded up to the dword holding the batch's last byte: loads never leave
+// that dword, let alone the allocation.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(uint64_t base,
+                                                          uint64_t end) {
+  end = (end + 3u) & ~3ull;
+  const uint64_t n = end > base ? end - base : 0;
+  return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0,
+                                           (int)(n < kOOB ? n : kOOB), 0x00020000);
+}
+
+template <bool NT>
+__device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  // aux bit 1 = nt: packet bytes are read exactly once
+  const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, NT ? 2 : 0);
+  return make_uint4(t.x, t.y, t.z, t.w);
+}
+
+__device__ __forceinline__ uint32_t bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+
+// ---------------------------------------------------------------------
+// Junk: the bytes of the (at most four) edge dwords that a dword-granular
+// sum takes but the reference does not. Window coordinates (window base =
+// floor4(packet start)); sh = start & 3; E = sh + summed length.
+// ---------------------------------------------------------------------
+struct Junk {
+  uint32_t off[4];   // window-relative dword offsets (kOOB: none)
+  uint32_t mask[4];  // bytes to subtract
+};
+
+__device__ __forceinline__ Junk make_junk(uint32_t sh, uint32_t E, int mode) {
+  Junk j;
+  // head: bytes [0, sh) of dword 0 precede the packet
+  j.off[0] = sh ? 0u : kOOB;
+  j.mask[0] = (1u << (8u * sh)) - 1u;
+  // tail: bytes [E&3, 4) of dword floor4(E) follow it
+  const uint32_t et = E & 3u;
+  j.off[1] = et ? (E & ~3u) : kOOB;
+  j.mask[1] = ~((1u << (8u * et)) - 1u);
+  // TX field (Encode writes 0 there): [fr, fr+2), maybe across two dwords
+  const uint32_t f = mode_field(mode);
+  const bool fld = mode_is_tx(mode) && sh + f + 2u <= E;
+  const uint32_t fr = sh + f;
+  const uint32_t fb = fr & 3u;
+  j.off[2] = fld ? (fr & ~3u) : kOOB;
+  j.mask[2] = fb == 3u ? 0xFF000000u : (0xFFFFu << (8u * fb));
+  j.off[3] = (fld && fb == 3u) ? (fr & ~3u) + 4u : kOOB;
+  j.mask[3] = 0xFFu;
+  return j;
+}
+
+template <bool BE>
+__device__ __forceinline__ uint32_t junk_sum(const uint32_t (&x)[4],
+                                             const Junk &j, uint32_t sel) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s = add_word<BE>(x[k] & j.mask[k], sel, s);
+  return s;
+}
+
+// ---------------------------------------------------------------------
+// Per-packet side data (uint16 initial or the 8-byte {src,dst} record),
+// fetched together with the packet bytes so the epilogue never waits on a
+// dependent load. Absent arrays read a zero word with stride 0, so the side
+// loads are unconditional too.
+// ---------------------------------------------------------------------
+__device__ uint32_t g_side_zero[2] = {0u, 0u};
+
+struct Side {
+  uint32_t a, b, i;
+};
+
+struct SidePtrs {
+  const uint8_t *a;
+  const uint8_t *i;
+  uint32_t as, is;
+};
+
+__device__ __forceinline__ SidePtrs side_ptrs(const BatchArgs &A) {
+  SidePtrs s;
+  const bool use_addrs = A.addrs && mode_has_pseudo(A.mode);
+  s.a = use_addrs ? A.addrs : (const uint8_t *)g_side_zero;
+  s.as = use_addrs ? 8u : 0u;
+  s.i = A.initial_arr ? (const uint8_t *)A.initial_arr : (const uint8_t *)g_side_zero;
+  s.is = A.initial_arr ? 2u : 0u;
+  return s;
+}
+
+__device__ __forceinline__ Side load_side(const SidePtrs &sp, uint64_t p) {
+  const uint32_t *a = (const uint32_t *)(sp.a + p * sp.as);
+  Side s;
+  s.a = a[0];
+  s.b = a[1];
+  s.i = *(const uint16_t *)(sp.i + p * sp.is);
+  return s;
+}
+
+// Per-packet epilogue. `v` is the packet's word sum (exact uint32 for BE,
+// its residue for LE). Adds the non-payload terms of the reference
+// composition, folds, complements, stores (and optionally sets the field).
 __device__ __forceinline__ void finish_packet(const BatchArgs &A, uint64_t p,
                                               uint32_t v, uint64_t len,
-                                              uint8_t *pkt, uint32_t hdr_end) {
+                                              const Side &sd, uint8_t *pkt,
+                                              uint32_t hdr_end) {
   const int mode = A.mode;
   if (mode == YU_MODE_RAW) {
-    v += A.initial_arr ? (uint32_t)A.initial_arr[p] : A.initial;
+    v += A.initial_arr ? sd.i : A.initial;
   } else if (mode_has_pseudo(mode)) {
     uint32_t ph;
     if (A.addrs) {
       // PseudoHeaderChecksum(proto, src, dst): src/dst big-endian words + proto
-      const uint32_t *a = (const uint32_t *)(A.addrs + 8 * p);
-      ph = sadperm(a[0], kSelSwap, 0u);
-      ph = sadperm(a[1], kSelSwap, ph);
+      ph = sadperm(sd.a, kSelSwap, 0u);
+      ph = sadperm(sd.b, kSelSwap, ph);
       ph += mode_proto(mode);
     } else {
-      ph = A.initial_arr ? (uint32_t)A.initial_arr[p] : A.initial;
+      ph = A.initial_arr ? sd.i : A.initial;
     }
     // + Checksum(BE16(uint16(length))) — header/udp.go:70-72, tcp.go:168-170
     v += ph + (uint32_t)(len & 0xFFFFu);
@@ -252,10 +311,81 @@ __device__ __forceinline__ void finish_packet(const BatchArgs &A, uint64_t p,
   }
 }
 
+// Dwords of chunk c at window offset cr that start before E4 = ceil4(E)
+// (signed compare: lim[j] = E4 - 4j may be negative).
+template <bool BE>
+__device__ __forceinline__ uint32_t sum_masked(const uint4 &c, int cr,
+                                               const int (&lim)[4],
+                                               uint32_t sel, uint32_t acc) {
+  acc = add_word<BE>(cr < lim[0] ? c.x : 0u, sel, acc);
+  acc = add_word<BE>(cr < lim[1] ? c.y : 0u, sel, acc);
+  acc = add_word<BE>(cr < lim[2] ? c.z : 0u, sel, acc);
+  acc = add_word<BE>(cr < lim[3] ? c.w : 0u, sel, acc);
+  return acc;
+}
+
+template <bool BE>
+__device__ __forceinline__ uint32_t sum_full(const uint4 &c, uint32_t sel,
+                                             uint32_t acc) {
+  acc = add_word<BE>(c.x, sel, acc);
+  acc = add_word<BE>(c.y, sel, acc);
+  acc = add_word<BE>(c.z, sel, acc);
+  acc = add_word<BE>(c.w, sel, acc);
+  return acc;
+}
+
+// IPv4 modes: HeaderLength() = (b[0] & 0xf) * 4 (header/ipv4.go:91-93); b[0]
+// is byte sh of dword 0 of the window, held by the group's first lane.
+__device__ __forceinline__ uint32_t ipv4_hl(uint32_t w0, uint32_t sh) {
+  return ((w0 >> (8u * sh)) & 0xFu) * 4u;
+}
+
 // ---------------------------------------------------------------------
-// k_small<G, U>: uniform stride, whole packet window in one step.
+// k_small<G, U, NT>: uniform stride, whole packet window in one step,
+// software-pipelined: the loads of step t+1 are issued before step t is
+// summed, reduced and stored.
 // ---------------------------------------------------------------------
 template <int G, int U>
+struct SmallItem {
+  uint4 c[U];
+  uint32_t jx[4];  // junk dwords (group leader)
+  Side sd;
+  uint32_t sh, len;
+};
+
+// Fetch the windows of packets pb+gw (pb = the wave's first packet of the
+// step; pb >= n fetches nothing).
+template <int G, int U, bool NT>
+__device__ __forceinline__ void small_fetch(const BatchArgs &A,
+                                            const SidePtrs &sp, uint64_t pb,
+                                            uint32_t gw, uint32_t gl, bool ipv4,
+                                            SmallItem<G, U> &it) {
+  const uint64_t p = pb + gw;
+  const bool active = p < A.n;
+  const uint64_t data = (uint64_t)(uintptr_t)A.data;
+  const uint64_t base = uniform64((data + pb * A.stride) & ~3ull);
+  const uint64_t sabs = data + (active ? p : pb) * A.stride;
+  const uint32_t lw = (uint32_t)((sabs & ~3ull) - base);  // this group's window
+  it.sh = (uint32_t)(sabs & 3u);
+  it.len = active ? A.len : 0u;
+  const uint32_t le = ipv4 ? (it.len < 60u ? it.len : 60u) : it.len;
+  const uint32_t eload = active ? it.sh + le : 0u;
+  const __amdgpu_buffer_rsrc_t r = rsrc_at(base, A.end);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t cr = 16u * (gl + (uint32_t)u * G);
+    it.c[u] = bld16<NT>(r, cr < eload ? lw + cr : kOOB);
+  }
+  // junk dwords: loaded by the group leader (IPv4 modes: after b[0] is known)
+  const bool lead = gl == G - 1 && active && !ipv4;
+  const Junk j = make_junk(it.sh, it.sh + it.len, A.mode);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    it.jx[k] = bld4(r, (lead && j.off[k] != kOOB) ? lw + j.off[k] : kOOB);
+  it.sd = load_side(sp, active ? p : A.n - 1);
+}
+
+template <int G, int U, bool NT>
 __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
   constexpr int GPW = 64 / G;
   const uint32_t lane = threadIdx.x & 63u;
@@ -263,55 +393,131 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
   const uint32_t gw = lane / G;
   const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
                         (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t step = (uint64_t)gridDim.x * (blockDim.x >> 6) * GPW;
   const int mode = A.mode;
   const bool ipv4 = mode_is_ipv4(mode);
+  const SidePtrs sp = side_ptrs(A);
+  const uint32_t uf = A.uf;
 
-  for (uint64_t pb = wave * GPW; pb < A.n; pb += nwave * GPW) {
-    const uint64_t p = pb + gw;
-    const bool active = p < A.n;
-    const uint64_t soff = active ? p * A.stride : 0;
-    const uintptr_t sabs = (uintptr_t)A.data + soff;
-    const uint8_t *wbase = (const uint8_t *)(sabs & ~(uintptr_t)15);
-    const uint32_t s = (uint32_t)(sabs & 15u);
-    const uint32_t len = active ? A.len : 0u;
-    const uint32_t eload = s + (ipv4 ? (len < 60u ? len : 60u) : len);
+  uint64_t pb = wave * GPW;
+  if (pb >= A.n) return;
+  SmallItem<G, U> it;
+  small_fetch<G, U, NT>(A, sp, pb, gw, gl, ipv4, it);
+  for (;;) {
+    const uint64_t pn = pb + step;
+    const bool more = pn < A.n;  // wave-uniform
+    SmallItem<G, U> nx;
+    small_fetch<G, U, NT>(A, sp, more ? pn : A.n, gw, gl, ipv4, nx);
 
-    uint4 c[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t cr = 16u * (gl + (uint32_t)u * G);
-      if (cr < eload)
-        c[u] = *(const uint4 *)(wbase + cr);
-      else
-        c[u] = make_uint4(0u, 0u, 0u, 0u);
-    }
-
-    uint32_t e = s + len;
+    uint32_t E = it.sh + it.len;
     if (ipv4) {
-      // HeaderLength() = (b[0] & 0xf) * 4 — header/ipv4.go:91-93
-      uint32_t b0 = (gl == 0 && len > 0) ? byte_of(c[0], s) : 0u;
-      b0 = __shfl(b0, (int)(lane & ~(uint32_t)(G - 1)), 64);
-      const uint32_t hl = (b0 & 0xFu) * 4u;
-      e = s + (len < hl ? len : hl);
+      const uint32_t hl = __shfl(ipv4_hl(it.c[0].x, it.sh), (int)(lane & ~(uint32_t)(G - 1)), 64);
+      E = it.sh + (it.len < hl ? it.len : hl);
     }
-    const Geom g = make_geom(s, e, mode);
-
+    const int E4 = (int)((E + 3u) & ~3u);
+    const int lim[4] = {E4, E4 - 4, E4 - 8, E4 - 12};
     uint32_t acc = 0;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      sum_chunk(c[u], 16u * (gl + (uint32_t)u * G), g, acc);
-
-    acc = group_sum<G>(acc);
-    if (active && gl == 0)
-      finish_packet(A, p, acc, len, A.fill ? A.fill + soff : nullptr, e - s);
+    for (int u = 0; u < U; ++u) {
+      const int cr = 16 * (int)(gl + (uint32_t)u * G);
+      if ((uint32_t)u < uf)
+        acc = sum_full<false>(it.c[u], 0u, acc);
+      else
+        acc = sum_masked<false>(it.c[u], cr, lim, 0u, acc);
+    }
+    acc = group_total<G>(acc);
+    const uint64_t p = pb + gw;
+    if (ipv4) {  // late junk: the tail depends on the header length
+      const uint64_t base = uniform64(((uint64_t)(uintptr_t)A.data + pb * A.stride) & ~3ull);
+      const uint64_t sabs = (uint64_t)(uintptr_t)A.data + (p < A.n ? p : pb) * A.stride;
+      const uint32_t lw = (uint32_t)((sabs & ~3ull) - base);
+      const __amdgpu_buffer_rsrc_t r = rsrc_at(base, A.end);
+      const Junk j = make_junk(it.sh, E, mode);
+      const bool lead = gl == G - 1 && p < A.n;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        it.jx[k] = bld4(r, (lead && j.off[k] != kOOB) ? lw + j.off[k] : kOOB);
+    }
+    if (gl == G - 1 && p < A.n) {
+      const Junk j = make_junk(it.sh, E, mode);
+      const uint32_t v = le_to_be(acc - junk_sum<false>(it.jx, j, 0u), it.sh & 1u);
+      finish_packet(A, p, v, it.len, it.sd,
+                    A.fill ? A.fill + p * A.stride : nullptr, E - it.sh);
+    }
+    if (!more) break;
+    it = nx;
+    pb = pn;
   }
 }
 
 // ---------------------------------------------------------------------
-// k_loop<U>: one wave per packet, 64*U*16-byte windows (ragged / large).
+// k_loop<U, NT, BE>: one wave per packet, 64*U*16-byte windows (ragged /
+// large packets). The wave walks a stream of (packet, window) items and
+// always issues the loads of the next item — the next window of this
+// packet, or the first window, junk dwords and side data of its next packet
+// (whose offsets were read one packet ahead) — before it sums the current.
 // ---------------------------------------------------------------------
-template <int U>
+struct LoopPkt {
+  uint64_t soff, len;
+  uint64_t base;  // floor4(packet start) as an address
+  uint32_t sh, E, eload;
+};
+
+__device__ __forceinline__ void loop_pkt(const BatchArgs &A, uint64_t p,
+                                         bool ipv4, LoopPkt &k) {
+  if (p >= A.n) {  // no packet: every load of it is out of range
+    k.soff = 0;
+    k.len = 0;
+    k.base = (uint64_t)(uintptr_t)A.data & ~3ull;
+    k.sh = 0;
+    k.E = 0;
+    k.eload = 0;
+    return;
+  }
+  if (A.offsets) {
+    k.soff = A.offsets[p];
+    k.len = A.offsets[p + 1] - k.soff;
+  } else {
+    k.soff = p * A.stride;
+    k.len = A.len;
+  }
+  const uint64_t sabs = (uint64_t)(uintptr_t)A.data + k.soff;
+  k.base = sabs & ~3ull;
+  k.sh = (uint32_t)(sabs & 3u);
+  const uint32_t l32 = (uint32_t)k.len;
+  k.E = k.sh + l32;
+  k.eload = k.sh + (ipv4 ? (l32 < 60u ? l32 : 60u) : l32);
+}
+
+// Loads of window [wb, wb + 64*U*16) of packet k.
+template <int U, bool NT>
+__device__ __forceinline__ void loop_fetch(const LoopPkt &k, uint32_t wb,
+                                           uint32_t lane, uint64_t end,
+                                           uint4 (&c)[U]) {
+  const __amdgpu_buffer_rsrc_t r = rsrc_at(uniform64(k.base + wb), end);
+  const uint32_t lim = k.eload > wb ? k.eload - wb : 0u;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t cr = 16u * (lane + 64u * (uint32_t)u);
+    c[u] = bld16<NT>(r, cr < lim ? cr : kOOB);
+  }
+}
+
+// Junk dwords of packet k (lane 63 only), each through its own descriptor so
+// packets of any length work.
+__device__ __forceinline__ void loop_junk(const LoopPkt &k, const Junk &j,
+                                          bool lead, uint64_t end,
+                                          uint32_t (&x)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const bool has = j.off[q] != kOOB;
+    const __amdgpu_buffer_rsrc_t r =
+        rsrc_at(uniform64(k.base + (has ? j.off[q] : 0u)), end);
+    x[q] = bld4(r, (lead && has) ? 0u : kOOB);
+  }
+}
+
+template <int U, bool NT, bool BE>
 __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
   constexpr uint32_t W = 64u * 16u * U;
   const uint32_t lane = threadIdx.x & 63u;
@@ -320,49 +526,79 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
   const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const int mode = A.mode;
   const bool ipv4 = mode_is_ipv4(mode);
+  const SidePtrs sp = side_ptrs(A);
+  const bool lead = lane == 63;
+  const uint64_t end = A.offsets ? (uint64_t)(uintptr_t)A.data + A.offsets[A.n] : A.end;
 
-  for (uint64_t p = wave; p < A.n; p += nwave) {
-    uint64_t soff, len;
-    if (A.offsets) {
-      soff = A.offsets[p];
-      len = A.offsets[p + 1] - soff;
-    } else {
-      soff = p * A.stride;
-      len = A.len;
+  uint64_t p = wave;
+  if (p >= A.n) return;
+  LoopPkt cur, nxt;
+  loop_pkt(A, p, ipv4, cur);
+  Side sd = load_side(sp, p);
+  uint32_t jx[4];
+  loop_junk(cur, make_junk(cur.sh, cur.E, mode), lead && !ipv4, end, jx);
+  uint64_t pn = p + nwave;
+  loop_pkt(A, pn, ipv4, nxt);
+
+  uint32_t wb = 0;
+  uint4 c[U];
+  loop_fetch<U, NT>(cur, 0, lane, end, c);
+  uint32_t acc = 0;
+  for (;;) {
+    const bool last = wb + W >= cur.eload;  // wave-uniform
+    const bool more = !last || pn < A.n;
+    // the next item: window wb+W of this packet, or window 0 of packet pn
+    uint4 cn[U];
+    loop_fetch<U, NT>(last ? nxt : cur, last ? 0u : wb + W, lane, end, cn);
+    const Side sdn = load_side(sp, (last && pn < A.n) ? pn : p);
+    uint32_t jxn[4];
+    loop_junk(nxt, make_junk(nxt.sh, nxt.E, mode), lead && last && !ipv4, end, jxn);
+
+    uint32_t E = cur.E;
+    if (ipv4) {  // single window: eload <= 63 < W
+      const uint32_t hl = __shfl(ipv4_hl(c[0].x, cur.sh), 0, 64);
+      const uint32_t l32 = (uint32_t)cur.len;
+      E = cur.sh + (l32 < hl ? l32 : hl);
     }
-    const uintptr_t sabs = (uintptr_t)A.data + soff;
-    const uint8_t *wbase = (const uint8_t *)(sabs & ~(uintptr_t)15);
-    const uint32_t s = (uint32_t)(sabs & 15u);
-    const uint32_t len32 = (uint32_t)len;
-    const uint32_t eload = s + (ipv4 ? (len32 < 60u ? len32 : 60u) : len32);
-
-    uint32_t e = s + len32;
-    Geom g = make_geom(s, e, mode);
-    uint32_t acc = 0;
-    for (uint32_t wb = 0; wb < eload; wb += W) {
-      uint4 c[U];
+    const uint32_t sel = (cur.sh & 1u) ? kSelIdent : kSelSwap;
+    const uint32_t E4 = (E + 3u) & ~3u;
+    if (wb + W <= E4) {  // full window (wave-uniform)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t cr = wb + 16u * (lane + 64u * (uint32_t)u);
-        if (cr < eload)
-          c[u] = *(const uint4 *)(wbase + cr);
-        else
-          c[u] = make_uint4(0u, 0u, 0u, 0u);
-      }
-      if (ipv4) {  // single window (eload <= 75 < W)
-        uint32_t b0 = (lane == 0 && len32 > 0) ? byte_of(c[0], s) : 0u;
-        b0 = __shfl(b0, 0, 64);
-        const uint32_t hl = (b0 & 0xFu) * 4u;
-        e = s + (len32 < hl ? len32 : hl);
-        g = make_geom(s, e, mode);
-      }
+      for (int u = 0; u < U; ++u) acc = sum_full<BE>(c[u], sel, acc);
+    } else {
+      const int e4 = (int)(E4 - wb);
+      const int lim[4] = {e4, e4 - 4, e4 - 8, e4 - 12};
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        sum_chunk(c[u], wb + 16u * (lane + 64u * (uint32_t)u), g, acc);
+        acc = sum_masked<BE>(c[u], 16 * (int)(lane + 64u * (uint32_t)u), lim, sel, acc);
     }
-    acc = group_sum<64>(acc);
-    if (lane == 0)
-      finish_packet(A, p, acc, len, A.fill ? A.fill + soff : nullptr, e - s);
+
+    if (last) {
+      acc = group_total<64>(acc);
+      const Junk j = make_junk(cur.sh, E, mode);
+      if (ipv4) loop_junk(cur, j, lead, end, jx);  // late: depends on IHL
+      if (lead) {
+        const uint32_t s = acc - junk_sum<BE>(jx, j, sel);
+        const uint32_t v = BE ? s : le_to_be(s, cur.sh & 1u);
+        finish_packet(A, p, v, cur.len, sd, A.fill ? A.fill + cur.soff : nullptr,
+                      E - cur.sh);
+      }
+      if (!more) break;
+      // advance to the next packet; read the offsets of the one after it
+      p = pn;
+      cur = nxt;
+      sd = sdn;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) jx[q] = jxn[q];
+      pn = p + nwave;
+      loop_pkt(A, pn, ipv4, nxt);
+      wb = 0;
+      acc = 0;
+    } else {
+      wb += W;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = cn[u];
   }
 }
 
@@ -374,46 +610,34 @@ typedef void (*KernelFn)(BatchArgs);
 struct Variant {
   const char *name;
   uint32_t window;  // bytes covered per packet step (0 = loop kernel)
-  KernelFn fn;
-  uint32_t packets_per_wave;
+  KernelFn fn[2];   // [plain loads, non-temporal loads]
+  uint32_t G;       // lanes per packet
 };
 
+#define YU_SMALL(G, U) \
+  {"k_small<" #G "," #U ">", 16u * G * U, {k_small<G, U, false>, k_small<G, U, true>}, G}
+
+// Ordered by window; for each window the variant with the most packets per
+// wave comes first (amortises the per-packet epilogue over more bytes).
 const Variant kSmall[] = {
-    {"k_small<4,1>", 64, k_small<4, 1>, 16},
-    {"k_small<8,1>", 128, k_small<8, 1>, 8},
-    {"k_small<16,1>", 256, k_small<16, 1>, 4},
-    {"k_small<32,1>", 512, k_small<32, 1>, 2},
-    {"k_small<64,1>", 1024, k_small<64, 1>, 1},
-    {"k_small<32,3>", 1536, k_small<32, 3>, 2},
-    {"k_small<64,2>", 2048, k_small<64, 2>, 1},
-    {"k_small<64,3>", 3072, k_small<64, 3>, 1},
-    {"k_small<64,4>", 4096, k_small<64, 4>, 1},
+    YU_SMALL(4, 1),  YU_SMALL(8, 1),  YU_SMALL(8, 2),  YU_SMALL(16, 2),
+    YU_SMALL(16, 3), YU_SMALL(16, 4), YU_SMALL(16, 6), YU_SMALL(32, 4),
+    YU_SMALL(32, 6), YU_SMALL(64, 4),
 };
-const Variant kLoop = {"k_loop<4>", 0, k_loop<4>, 1};
+const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, false, false>, k_loop<4, true, false>}, 64};
+const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, false, true>, k_loop<4, true, true>}, 64};
 
-uint64_t gcd64(uint64_t a, uint64_t b) {
-  while (b) {
-    uint64_t t = a % b;
-    a = b;
-    b = t;
-  }
-  return a;
-}
-
-// Largest (start & 15) over the batch's packet starts.
-uint32_t max_misalign(uint64_t base_mod16, uint64_t stride, uint64_t n) {
-  if (n <= 1) return (uint32_t)(base_mod16 & 15u);
-  uint64_t g = gcd64(stride & 15u ? (stride & 15u) : 16u, 16u);
-  return (uint32_t)((base_mod16 % g) + (16u - g));
-}
-
-const Variant &pick_uniform(uint64_t base_mod16, uint64_t stride, uint32_t len,
+const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
                             uint64_t n, int mode) {
-  uint64_t need = mode_is_ipv4(mode) ? (len < 60u ? len : 60u) : len;
-  uint64_t span = need + max_misalign(base_mod16, stride, n);
-  for (const Variant &v : kSmall)
-    if (span <= v.window) return v;
-  return kLoop;
+  const uint64_t need = mode_is_ipv4(mode) ? (len < 60u ? len : 60u) : len;
+  // the window starts at floor4(start): up to 3 extra bytes in front
+  const bool aligned4 = ((base | (n > 1 ? stride : 0)) & 3u) == 0;
+  const uint64_t span = need + (aligned4 ? 0 : 3);
+  for (const Variant &v : kSmall) {
+    // lane window offsets are 32-bit: (64/G - 1) strides + the window
+    if (span <= v.window && (64u / v.G) * stride + v.window < kOOB) return v;
+  }
+  return len > kLEMax ? kLoopBE : kLoopLE;
 }
 
 std::atomic<int> g_cu_count[64];
@@ -430,12 +654,22 @@ int cu_count(int dev) {
   return c;
 }
 
+// Tuning knobs (read once). YU_BLOCKS_PER_CU: persistent-grid size in
+// 256-thread blocks per CU; YU_NT: 0 selects plain loads for packet bytes.
+int env_int(const char *name, int lo, int hi, int dflt) {
+  const char *s = getenv(name);
+  if (!s || !*s) return dflt;
+  int x = atoi(s);
+  return (x >= lo && x <= hi) ? x : dflt;
+}
+
 int blocks_per_cu() {
-  static int v = [] {
-    const char *s = getenv("YU_BLOCKS_PER_CU");
-    int x = s ? atoi(s) : 0;
-    return (x >= 1 && x <= 32) ? x : 8;
-  }();
+  static int v = env_int("YU_BLOCKS_PER_CU", 1, 32, 8);
+  return v;
+}
+
+int use_nt() {
+  static int v = env_int("YU_NT", 0, 1, 1);
   return v;
 }
 
@@ -451,12 +685,13 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_status(e);
   const uint64_t waves_per_block = 4;
-  uint64_t waves = (A.n + v.packets_per_wave - 1) / v.packets_per_wave;
+  const uint64_t ppw = 64u / v.G;
+  uint64_t waves = (A.n + ppw - 1) / ppw;
   uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
   uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu();
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(v.fn, dim3((unsigned)blocks), dim3(256), 0, stream, A);
+  hipLaunchKernelGGL(v.fn[use_nt()], dim3((unsigned)blocks), dim3(256), 0, stream, A);
   return hip_status(hipGetLastError());
 }
 
@@ -482,10 +717,13 @@ int batch_uniform(const uint8_t *data, uint8_t *fill, uint64_t stride,
   int rc = check_common(mode, initial_arr, addrs, out, fill != nullptr);
   if (rc) return rc;
   if (n == 0) return YU_OK;
-  if (!data && len) return YU_EINVAL;
+  if (!data) return YU_EINVAL;
   if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
   if (len < min_len(mode)) return YU_EINVAL;
   if (len >= 0xFFFFFFF0u) return YU_EINVAL;
+  // fill: packets must start 4-byte aligned (no dword shared with a
+  // neighbour's field)
+  if (fill && (((uintptr_t)data | stride) & 3u)) return YU_EINVAL;
   BatchArgs A;
   A.data = data;
   A.offsets = nullptr;
@@ -495,10 +733,12 @@ int batch_uniform(const uint8_t *data, uint8_t *fill, uint64_t stride,
   A.fill = fill;
   A.stride = stride;
   A.n = n;
+  A.end = (uint64_t)(uintptr_t)data + (n - 1) * stride + len;
   A.len = len;
   A.initial = initial;
   A.mode = mode;
-  const Variant &v = pick_uniform((uintptr_t)data & 15u, stride, len, n, mode);
+  const Variant &v = pick_uniform((uintptr_t)data, stride, len, n, mode);
+  A.uf = v.window ? (mode_is_ipv4(mode) ? 0u : len / (16u * v.G)) : 0u;
   return launch(v, A, (hipStream_t)stream);
 }
 
@@ -519,10 +759,14 @@ int batch_ragged(const uint8_t *data, uint8_t *fill, const uint64_t *offsets,
   A.fill = fill;
   A.stride = 0;
   A.n = n;
+  A.end = 0;
   A.len = 0;
   A.initial = initial;
+  A.uf = 0;
   A.mode = mode;
-  return launch(kLoop, A, (hipStream_t)stream);
+  // RAW packets may exceed 131072 bytes: the exact BE sum; transport/IPv4/
+  // ICMP packets are <= 65535 bytes by contract: the LE sum.
+  return launch(mode == YU_MODE_RAW ? kLoopBE : kLoopLE, A, (hipStream_t)stream);
 }
 
 }  // namespace
@@ -558,6 +802,8 @@ int yu_csum_fill_ragged(uint8_t *data, const uint64_t *offsets, uint64_t n,
                         int mode, const uint16_t *initial_arr,
                         uint16_t initial, const uint8_t *addrs, uint16_t *out,
                         void *stream) {
+  // contract (include/yucsum.h): offsets are multiples of 4, data 4-aligned
+  if ((uintptr_t)data & 3u) return YU_EINVAL;
   return batch_ragged(data, data, offsets, n, mode, initial_arr, initial,
                       addrs, out, stream);
 }
