@@ -113,7 +113,7 @@ class Workload:
 
     def kernel_name(self) -> str:
         if self.offsets is not None:
-            return "k_loop<4>"
+            return "k_loop<4,BE>" if self.mode == batch.RAW else "k_loop<4,LE>"
         return batch.variant(self.L, self.L, self.mode, self.data[0].data_ptr() & 15)
 
 
@@ -198,7 +198,7 @@ def host_threads() -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -226,11 +226,16 @@ def main():
     value = world * w.bytes * args.steps / wall_max / GIB
     achieved = w.bytes / kern / 1e9  # GB/s (decimal, like the peak)
 
-    traffic = None
+    # HBM bytes per launch from rocprofv3 PMC passes of this same command
+    # (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from
+    # tools/profile.sh output: 2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes).
+    traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get(f"config{args.config}")
+            rec = json.load(open(tf)).get(f"config{args.config}")
+            if rec and rec.get("kernel") == w.kernel_name():
+                traffic, traffic_src = rec["hbm_bytes_per_launch"], rec["source"]
         except Exception:
             traffic = None
 
@@ -264,6 +269,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes": w.bytes,
             "kernel_avg_us": round(kern * 1e6, 2),
         },
     }

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round profile (run on the GPU box): rocprofv3 kernel trace + stats of the
+# bench command, then separate PMC passes for FETCH_SIZE and WRITE_SIZE (never
+# combined with sys/runtime traces). Output under gpurun_out/prof_<tag>.
+set -euo pipefail
+TAG=${1:-r01}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp
+export TMPDIR=/tmp
+for cfg in 3 2 4; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c$cfg" -o run -- \
+    python3 "$ROOT/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --no-extra \
+    > "$OUT/bench_c${cfg}_under_trace.json"
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_${ctr}_c$cfg" -o run -- \
+      python3 "$ROOT/bench.py" --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-extra \
+      > "$OUT/bench_c${cfg}_pmc_$ctr.json"
+  done
+done
+echo done > "$OUT/DONE"

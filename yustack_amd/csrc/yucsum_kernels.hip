@@ -34,8 +34,9 @@
 // iff they start before e. The few bytes this gets wrong — up to 3 bytes
 // before an unaligned s, up to 3 after an unaligned e, and in TX modes the
 // two checksum-field bytes that Encode() zeroes — sit in at most four known
-// dwords; the group leader loads those dwords once more (same cache lines)
-// and subtracts their masked bytes.
+// dwords; the group leader gathers them (head and field from the registers of
+// the lanes holding them, an unaligned tail by one extra dword load) and
+// subtracts their masked bytes. No byte is loaded twice.
 //
 // Loads go through buffer descriptors based at wave-uniform addresses: a lane
 // that must not load passes an out-of-range offset and gets zeros without a
@@ -50,7 +51,8 @@
 //     log2(G) DPP adds and its last lane finishes the packet.
 //   k_loop<U, BE>: one wave per packet, looping over 64*U*16-byte windows, for
 //     ragged (tun-style, any alignment) batches and uniform packets > 4 KiB.
-//   Both are persistent grid-stride kernels sized to the CU count.
+//   Both are grid-stride kernels; the grid is sized per CU and over-subscribed
+//   (see blocks_per_cu).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -195,18 +197,18 @@ __device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return make_uint4(t.x, t.y, t.z, t.w);
 }
 
-__device__ __forceinline__ uint32_t bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
-}
-
 // ---------------------------------------------------------------------
 // Junk: the bytes of the (at most four) edge dwords that a dword-granular
 // sum takes but the reference does not. Window coordinates (window base =
 // floor4(packet start)); sh = start & 3; E = sh + summed length.
 // ---------------------------------------------------------------------
+// Items 0 (head) and 2/3 (field) always lie in the window's first 24 bytes,
+// i.e. in chunk 0 or 1 of step u = 0: they are taken from the registers of
+// the lanes holding them (junk_from_regs). Item 1 (tail) can be anywhere and
+// is re-loaded (only when the packet ends off a dword boundary).
 struct Junk {
   uint32_t off[4];   // window-relative dword offsets (kOOB: none)
-  uint32_t mask[4];  // bytes to subtract
+  uint32_t mask[4];  // bytes to subtract (0 when the item is absent)
 };
 
 __device__ __forceinline__ Junk make_junk(uint32_t sh, uint32_t E, int mode) {
@@ -217,17 +219,58 @@ __device__ __forceinline__ Junk make_junk(uint32_t sh, uint32_t E, int mode) {
   // tail: bytes [E&3, 4) of dword floor4(E) follow it
   const uint32_t et = E & 3u;
   j.off[1] = et ? (E & ~3u) : kOOB;
-  j.mask[1] = ~((1u << (8u * et)) - 1u);
+  j.mask[1] = et ? ~((1u << (8u * et)) - 1u) : 0u;
   // TX field (Encode writes 0 there): [fr, fr+2), maybe across two dwords
   const uint32_t f = mode_field(mode);
   const bool fld = mode_is_tx(mode) && sh + f + 2u <= E;
   const uint32_t fr = sh + f;
   const uint32_t fb = fr & 3u;
   j.off[2] = fld ? (fr & ~3u) : kOOB;
-  j.mask[2] = fb == 3u ? 0xFF000000u : (0xFFFFu << (8u * fb));
-  j.off[3] = (fld && fb == 3u) ? (fr & ~3u) + 4u : kOOB;
-  j.mask[3] = 0xFFu;
+  j.mask[2] = !fld ? 0u : (fb == 3u ? 0xFF000000u : (0xFFFFu << (8u * fb)));
+  const bool f2 = fld && fb == 3u;
+  j.off[3] = f2 ? (fr & ~3u) + 4u : kOOB;
+  j.mask[3] = f2 ? 0xFFu : 0u;
   return j;
+}
+
+__device__ __forceinline__ uint32_t pick_dword(const uint4 &c, uint32_t q) {
+  return q == 0 ? c.x : (q == 1 ? c.y : (q == 2 ? c.z : c.w));
+}
+
+// The dword at window offset d of the group whose first lane is `gbase`
+// (G = 1 << LG lanes, chunk k = d/16 held by lane gbase + k%G in step k/G),
+// read from that lane's registers. Every lane offers the dword its own group
+// asks for, so all lanes must execute it.
+template <int U, int LG>
+__device__ __forceinline__ uint32_t take_dword(const uint4 (&c)[U], uint32_t d,
+                                               uint32_t gbase) {
+  const uint32_t k = d >> 4;
+  const uint32_t u = k >> LG;
+  const uint32_t q = (d >> 2) & 3u;
+  uint32_t w = pick_dword(c[0], q);
+#pragma unroll
+  for (int i = 1; i < U; ++i) w = (u == (uint32_t)i) ? pick_dword(c[i], q) : w;
+  return __shfl(w, (int)(gbase + (k & ((1u << LG) - 1u))), 64);
+}
+
+// Head and field junk dwords (items 0, 2, 3): always in chunk 0 or 1, i.e. in
+// step 0 for any G >= 2.
+template <int U, int LG>
+__device__ __forceinline__ void junk_head_field(const uint4 (&c)[U], uint32_t gbase,
+                                                const Junk &j, uint32_t (&x)[4]) {
+  const uint4 c0[1] = {c[0]};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k == 1) continue;
+    x[k] = take_dword<1, LG>(c0, j.off[k] == kOOB ? 0u : j.off[k], gbase);
+  }
+}
+
+// Tail junk dword (item 1), `wb` = window offset of the registers' window.
+template <int U, int LG>
+__device__ __forceinline__ uint32_t junk_tail(const uint4 (&c)[U], uint32_t gbase,
+                                              const Junk &j, uint32_t wb) {
+  return take_dword<U, LG>(c, j.off[1] == kOOB ? 0u : j.off[1] - wb, gbase);
 }
 
 template <bool BE>
@@ -348,7 +391,6 @@ __device__ __forceinline__ uint32_t ipv4_hl(uint32_t w0, uint32_t sh) {
 template <int G, int U>
 struct SmallItem {
   uint4 c[U];
-  uint32_t jx[4];  // junk dwords (group leader)
   Side sd;
   uint32_t sh, len;
 };
@@ -376,12 +418,6 @@ __device__ __forceinline__ void small_fetch(const BatchArgs &A,
     const uint32_t cr = 16u * (gl + (uint32_t)u * G);
     it.c[u] = bld16<NT>(r, cr < eload ? lw + cr : kOOB);
   }
-  // junk dwords: loaded by the group leader (IPv4 modes: after b[0] is known)
-  const bool lead = gl == G - 1 && active && !ipv4;
-  const Junk j = make_junk(it.sh, it.sh + it.len, A.mode);
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    it.jx[k] = bld4(r, (lead && j.off[k] != kOOB) ? lw + j.off[k] : kOOB);
   it.sd = load_side(sp, active ? p : A.n - 1);
 }
 
@@ -427,20 +463,14 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
     }
     acc = group_total<G>(acc);
     const uint64_t p = pb + gw;
-    if (ipv4) {  // late junk: the tail depends on the header length
-      const uint64_t base = uniform64(((uint64_t)(uintptr_t)A.data + pb * A.stride) & ~3ull);
-      const uint64_t sabs = (uint64_t)(uintptr_t)A.data + (p < A.n ? p : pb) * A.stride;
-      const uint32_t lw = (uint32_t)((sabs & ~3ull) - base);
-      const __amdgpu_buffer_rsrc_t r = rsrc_at(base, A.end);
-      const Junk j = make_junk(it.sh, E, mode);
-      const bool lead = gl == G - 1 && p < A.n;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        it.jx[k] = bld4(r, (lead && j.off[k] != kOOB) ? lw + j.off[k] : kOOB);
-    }
+    constexpr int LG = __builtin_ctz(G);
+    const uint32_t gbase = lane & ~(uint32_t)(G - 1);
+    const Junk j = make_junk(it.sh, E, mode);
+    uint32_t jx[4];
+    junk_head_field<U, LG>(it.c, gbase, j, jx);
+    jx[1] = junk_tail<U, LG>(it.c, gbase, j, 0u);
     if (gl == G - 1 && p < A.n) {
-      const Junk j = make_junk(it.sh, E, mode);
-      const uint32_t v = le_to_be(acc - junk_sum<false>(it.jx, j, 0u), it.sh & 1u);
+      const uint32_t v = le_to_be(acc - junk_sum<false>(jx, j, 0u), it.sh & 1u);
       finish_packet(A, p, v, it.len, it.sd,
                     A.fill ? A.fill + p * A.stride : nullptr, E - it.sh);
     }
@@ -454,7 +484,7 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
 // k_loop<U, NT, BE>: one wave per packet, 64*U*16-byte windows (ragged /
 // large packets). The wave walks a stream of (packet, window) items and
 // always issues the loads of the next item — the next window of this
-// packet, or the first window, junk dwords and side data of its next packet
+// packet, or the first window and side data of its next packet
 // (whose offsets were read one packet ahead) — before it sums the current.
 // ---------------------------------------------------------------------
 struct LoopPkt {
@@ -503,20 +533,6 @@ __device__ __forceinline__ void loop_fetch(const LoopPkt &k, uint32_t wb,
   }
 }
 
-// Junk dwords of packet k (lane 63 only), each through its own descriptor so
-// packets of any length work.
-__device__ __forceinline__ void loop_junk(const LoopPkt &k, const Junk &j,
-                                          bool lead, uint64_t end,
-                                          uint32_t (&x)[4]) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const bool has = j.off[q] != kOOB;
-    const __amdgpu_buffer_rsrc_t r =
-        rsrc_at(uniform64(k.base + (has ? j.off[q] : 0u)), end);
-    x[q] = bld4(r, (lead && has) ? 0u : kOOB);
-  }
-}
-
 template <int U, bool NT, bool BE>
 __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
   constexpr uint32_t W = 64u * 16u * U;
@@ -535,8 +551,7 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
   LoopPkt cur, nxt;
   loop_pkt(A, p, ipv4, cur);
   Side sd = load_side(sp, p);
-  uint32_t jx[4];
-  loop_junk(cur, make_junk(cur.sh, cur.E, mode), lead && !ipv4, end, jx);
+  uint32_t jx[4] = {0u, 0u, 0u, 0u};  // junk dwords: head/field at window 0, tail at the last
   uint64_t pn = p + nwave;
   loop_pkt(A, pn, ipv4, nxt);
 
@@ -551,8 +566,6 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
     uint4 cn[U];
     loop_fetch<U, NT>(last ? nxt : cur, last ? 0u : wb + W, lane, end, cn);
     const Side sdn = load_side(sp, (last && pn < A.n) ? pn : p);
-    uint32_t jxn[4];
-    loop_junk(nxt, make_junk(nxt.sh, nxt.E, mode), lead && last && !ipv4, end, jxn);
 
     uint32_t E = cur.E;
     if (ipv4) {  // single window: eload <= 63 < W
@@ -560,6 +573,8 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
       const uint32_t l32 = (uint32_t)cur.len;
       E = cur.sh + (l32 < hl ? l32 : hl);
     }
+    const Junk j = make_junk(cur.sh, E, mode);
+    if (wb == 0) junk_head_field<U, 6>(c, 0u, j, jx);
     const uint32_t sel = (cur.sh & 1u) ? kSelIdent : kSelSwap;
     const uint32_t E4 = (E + 3u) & ~3u;
     if (wb + W <= E4) {  // full window (wave-uniform)
@@ -575,8 +590,7 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
 
     if (last) {
       acc = group_total<64>(acc);
-      const Junk j = make_junk(cur.sh, E, mode);
-      if (ipv4) loop_junk(cur, j, lead, end, jx);  // late: depends on IHL
+      jx[1] = junk_tail<U, 6>(c, 0u, j, wb);
       if (lead) {
         const uint32_t s = acc - junk_sum<BE>(jx, j, sel);
         const uint32_t v = BE ? s : le_to_be(s, cur.sh & 1u);
@@ -588,8 +602,6 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
       p = pn;
       cur = nxt;
       sd = sdn;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) jx[q] = jxn[q];
       pn = p + nwave;
       loop_pkt(A, pn, ipv4, nxt);
       wb = 0;
@@ -627,16 +639,29 @@ const Variant kSmall[] = {
 const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, false, false>, k_loop<4, true, false>}, 64};
 const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, false, true>, k_loop<4, true, true>}, 64};
 
+// Tuning override (measurement only): YU_VARIANT=<name> forces a k_small
+// variant whenever it covers the shape.
+const char *forced_variant() {
+  static const char *v = getenv("YU_VARIANT");
+  return v;
+}
+
 const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
                             uint64_t n, int mode) {
   const uint64_t need = mode_is_ipv4(mode) ? (len < 60u ? len : 60u) : len;
   // the window starts at floor4(start): up to 3 extra bytes in front
   const bool aligned4 = ((base | (n > 1 ? stride : 0)) & 3u) == 0;
   const uint64_t span = need + (aligned4 ? 0 : 3);
-  for (const Variant &v : kSmall) {
-    // lane window offsets are 32-bit: (64/G - 1) strides + the window
-    if (span <= v.window && (64u / v.G) * stride + v.window < kOOB) return v;
+  // lane window offsets are 32-bit: (64/G - 1) strides + the window
+  auto fits = [&](const Variant &v) {
+    return span <= v.window && (64u / v.G) * stride + v.window < kOOB;
+  };
+  if (const char *f = forced_variant()) {
+    for (const Variant &v : kSmall)
+      if (strcmp(v.name, f) == 0 && fits(v)) return v;
   }
+  for (const Variant &v : kSmall)
+    if (fits(v)) return v;
   return len > kLEMax ? kLoopBE : kLoopLE;
 }
 
@@ -654,7 +679,7 @@ int cu_count(int dev) {
   return c;
 }
 
-// Tuning knobs (read once). YU_BLOCKS_PER_CU: persistent-grid size in
+// Tuning knobs (read once, measurement only). YU_BLOCKS_PER_CU: grid size in
 // 256-thread blocks per CU; YU_NT: 0 selects plain loads for packet bytes.
 int env_int(const char *name, int lo, int hi, int dflt) {
   const char *s = getenv(name);
@@ -663,9 +688,15 @@ int env_int(const char *name, int lo, int hi, int dflt) {
   return (x >= lo && x <= hi) ? x : dflt;
 }
 
-int blocks_per_cu() {
-  static int v = env_int("YU_BLOCKS_PER_CU", 1, 32, 8);
-  return v;
+// Grid size in 256-thread blocks per CU. The grid is deliberately larger than
+// what is resident at once (5-8 blocks/CU): finished blocks are replaced by
+// fresh ones, which evens out the per-CU tail. Measured optimum on MI355X
+// (tools/kbench, round 1): 64 for MTU-size and larger packets, 16 for the
+// tiny-packet variants (G < 16).
+int blocks_per_cu(uint32_t G) {
+  static int v = env_int("YU_BLOCKS_PER_CU", 1, 1024, 0);
+  if (v) return v;
+  return G < 16 ? 16 : 64;
 }
 
 int use_nt() {
@@ -688,7 +719,7 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   const uint64_t ppw = 64u / v.G;
   uint64_t waves = (A.n + ppw - 1) / ppw;
   uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
-  uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu();
+  uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu(v.G);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(v.fn[use_nt()], dim3((unsigned)blocks), dim3(256), 0, stream, A);
