@@ -34,9 +34,9 @@
 // iff they start before e. The few bytes this gets wrong — up to 3 bytes
 // before an unaligned s, up to 3 after an unaligned e, and in TX modes the
 // two checksum-field bytes that Encode() zeroes — sit in at most four known
-// dwords; the group leader gathers them (head and field from the registers of
-// the lanes holding them, an unaligned tail by one extra dword load) and
-// subtracts their masked bytes. No byte is loaded twice.
+// dwords; the group leader gathers them from the registers of the lanes
+// holding them (one cross-lane read each) and subtracts their masked bytes.
+// No byte is loaded twice.
 //
 // Loads go through buffer descriptors based at wave-uniform addresses: a lane
 // that must not load passes an out-of-range offset and gets zeros without a
@@ -190,46 +190,50 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(uint64_t base,
                                            (int)(n < kOOB ? n : kOOB), 0x00020000);
 }
 
-template <bool NT>
-__device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  // aux bit 1 = nt: packet bytes are read exactly once
-  const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, NT ? 2 : 0);
+// Load policy. Packet bytes are read once, and non-temporal (nt, aux bit 1)
+// loads stream them fastest, but an nt line does not stay in L2, so the line
+// two neighbouring packets share is fetched twice. NT = 0: plain loads;
+// 1: all nt; 2 (default): nt except the first and last step of a window,
+// which hold the shared lines.
+__device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t off,
+                                       bool nt) {
+  const u32x4 t = nt ? __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 2)
+                     : __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
   return make_uint4(t.x, t.y, t.z, t.w);
 }
 
+template <int NT>
+__device__ __forceinline__ constexpr bool nt_step(int u, int U) {
+  return NT == 1 || (NT == 2 && u != 0 && u != U - 1);
+}
+
 // ---------------------------------------------------------------------
-// Junk: the bytes of the (at most four) edge dwords that a dword-granular
-// sum takes but the reference does not. Window coordinates (window base =
-// floor4(packet start)); sh = start & 3; E = sh + summed length.
+// Junk: bytes of dwords the dword-granular sum includes but the reference
+// does not, other than the unaligned tail (masked in sum_masked). Window
+// coordinates (window base = floor4(packet start)); sh = start & 3; E = sh +
+// summed length. Item 0: the head bytes [0, sh) of dword 0; items 1/2: the
+// TX checksum field [sh+f, sh+f+2) (Encode writes 0 there), which may
+// straddle two dwords. All lie in the window's first 24 bytes, i.e. in chunk
+// 0 or 1 of step 0, and are read from the registers of the lanes holding
+// them — never with an extra load.
 // ---------------------------------------------------------------------
-// Items 0 (head) and 2/3 (field) always lie in the window's first 24 bytes,
-// i.e. in chunk 0 or 1 of step u = 0: they are taken from the registers of
-// the lanes holding them (junk_from_regs). Item 1 (tail) can be anywhere and
-// is re-loaded (only when the packet ends off a dword boundary).
 struct Junk {
-  uint32_t off[4];   // window-relative dword offsets (kOOB: none)
-  uint32_t mask[4];  // bytes to subtract (0 when the item is absent)
+  uint32_t off[3];   // window-relative dword offsets
+  uint32_t mask[3];  // bytes to subtract (0 when the item is absent)
 };
 
 __device__ __forceinline__ Junk make_junk(uint32_t sh, uint32_t E, int mode) {
   Junk j;
-  // head: bytes [0, sh) of dword 0 precede the packet
-  j.off[0] = sh ? 0u : kOOB;
-  j.mask[0] = (1u << (8u * sh)) - 1u;
-  // tail: bytes [E&3, 4) of dword floor4(E) follow it
-  const uint32_t et = E & 3u;
-  j.off[1] = et ? (E & ~3u) : kOOB;
-  j.mask[1] = et ? ~((1u << (8u * et)) - 1u) : 0u;
-  // TX field (Encode writes 0 there): [fr, fr+2), maybe across two dwords
+  j.off[0] = 0u;
+  j.mask[0] = (1u << (8u * sh)) - 1u;  // 0 for sh == 0
   const uint32_t f = mode_field(mode);
   const bool fld = mode_is_tx(mode) && sh + f + 2u <= E;
   const uint32_t fr = sh + f;
   const uint32_t fb = fr & 3u;
-  j.off[2] = fld ? (fr & ~3u) : kOOB;
-  j.mask[2] = !fld ? 0u : (fb == 3u ? 0xFF000000u : (0xFFFFu << (8u * fb)));
-  const bool f2 = fld && fb == 3u;
-  j.off[3] = f2 ? (fr & ~3u) + 4u : kOOB;
-  j.mask[3] = f2 ? 0xFFu : 0u;
+  j.off[1] = fr & ~3u;
+  j.mask[1] = !fld ? 0u : (fb == 3u ? 0xFF000000u : (0xFFFFu << (8u * fb)));
+  j.off[2] = (fr & ~3u) + 4u;
+  j.mask[2] = (fld && fb == 3u) ? 0xFFu : 0u;
   return j;
 }
 
@@ -237,48 +241,27 @@ __device__ __forceinline__ uint32_t pick_dword(const uint4 &c, uint32_t q) {
   return q == 0 ? c.x : (q == 1 ? c.y : (q == 2 ? c.z : c.w));
 }
 
-// The dword at window offset d of the group whose first lane is `gbase`
-// (G = 1 << LG lanes, chunk k = d/16 held by lane gbase + k%G in step k/G),
-// read from that lane's registers. Every lane offers the dword its own group
-// asks for, so all lanes must execute it.
-template <int U, int LG>
-__device__ __forceinline__ uint32_t take_dword(const uint4 (&c)[U], uint32_t d,
-                                               uint32_t gbase) {
-  const uint32_t k = d >> 4;
-  const uint32_t u = k >> LG;
-  const uint32_t q = (d >> 2) & 3u;
-  uint32_t w = pick_dword(c[0], q);
+// Junk dwords of the group whose first lane is `gbase` (G = 1 << LG lanes;
+// chunk k = off/16 is held by lane gbase + k in step 0; c0 = this lane's
+// step-0 chunk). Every lane offers the dword its own group asks for, so all
+// lanes must execute it.
+template <int LG>
+__device__ __forceinline__ void junk_take(const uint4 &c0, uint32_t gbase,
+                                          const Junk &j, uint32_t (&x)[3]) {
+  static_assert(LG >= 1, "junk chunks 0/1 must sit in different lanes of step 0");
 #pragma unroll
-  for (int i = 1; i < U; ++i) w = (u == (uint32_t)i) ? pick_dword(c[i], q) : w;
-  return __shfl(w, (int)(gbase + (k & ((1u << LG) - 1u))), 64);
-}
-
-// Head and field junk dwords (items 0, 2, 3): always in chunk 0 or 1, i.e. in
-// step 0 for any G >= 2.
-template <int U, int LG>
-__device__ __forceinline__ void junk_head_field(const uint4 (&c)[U], uint32_t gbase,
-                                                const Junk &j, uint32_t (&x)[4]) {
-  const uint4 c0[1] = {c[0]};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (k == 1) continue;
-    x[k] = take_dword<1, LG>(c0, j.off[k] == kOOB ? 0u : j.off[k], gbase);
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t d = j.off[k];
+    x[k] = __shfl(pick_dword(c0, (d >> 2) & 3u), (int)(gbase + (d >> 4)), 64);
   }
 }
 
-// Tail junk dword (item 1), `wb` = window offset of the registers' window.
-template <int U, int LG>
-__device__ __forceinline__ uint32_t junk_tail(const uint4 (&c)[U], uint32_t gbase,
-                                              const Junk &j, uint32_t wb) {
-  return take_dword<U, LG>(c, j.off[1] == kOOB ? 0u : j.off[1] - wb, gbase);
-}
-
 template <bool BE>
-__device__ __forceinline__ uint32_t junk_sum(const uint32_t (&x)[4],
+__device__ __forceinline__ uint32_t junk_sum(const uint32_t (&x)[3],
                                              const Junk &j, uint32_t sel) {
   uint32_t s = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) s = add_word<BE>(x[k] & j.mask[k], sel, s);
+  for (int k = 0; k < 3; ++k) s = add_word<BE>(x[k] & j.mask[k], sel, s);
   return s;
 }
 
@@ -354,16 +337,23 @@ __device__ __forceinline__ void finish_packet(const BatchArgs &A, uint64_t p,
   }
 }
 
-// Dwords of chunk c at window offset cr that start before E4 = ceil4(E)
-// (signed compare: lim[j] = E4 - 4j may be negative).
+// Chunk c at window offset cr, cut at the packet end E: dword j (window
+// offset cr + 4j) is whole if it ends by E, keeps its first E&3 bytes (tm) if
+// it straddles E, and is dropped otherwise. lim[j] = floor4(E) - 4j (signed:
+// may be negative).
+__device__ __forceinline__ uint32_t tail_cut(uint32_t x, int cr, int lim,
+                                             uint32_t tm) {
+  return cr < lim ? x : (cr == lim ? (x & tm) : 0u);
+}
+
 template <bool BE>
 __device__ __forceinline__ uint32_t sum_masked(const uint4 &c, int cr,
-                                               const int (&lim)[4],
+                                               const int (&lim)[4], uint32_t tm,
                                                uint32_t sel, uint32_t acc) {
-  acc = add_word<BE>(cr < lim[0] ? c.x : 0u, sel, acc);
-  acc = add_word<BE>(cr < lim[1] ? c.y : 0u, sel, acc);
-  acc = add_word<BE>(cr < lim[2] ? c.z : 0u, sel, acc);
-  acc = add_word<BE>(cr < lim[3] ? c.w : 0u, sel, acc);
+  acc = add_word<BE>(tail_cut(c.x, cr, lim[0], tm), sel, acc);
+  acc = add_word<BE>(tail_cut(c.y, cr, lim[1], tm), sel, acc);
+  acc = add_word<BE>(tail_cut(c.z, cr, lim[2], tm), sel, acc);
+  acc = add_word<BE>(tail_cut(c.w, cr, lim[3], tm), sel, acc);
   return acc;
 }
 
@@ -397,7 +387,7 @@ struct SmallItem {
 
 // Fetch the windows of packets pb+gw (pb = the wave's first packet of the
 // step; pb >= n fetches nothing).
-template <int G, int U, bool NT>
+template <int G, int U, int NT>
 __device__ __forceinline__ void small_fetch(const BatchArgs &A,
                                             const SidePtrs &sp, uint64_t pb,
                                             uint32_t gw, uint32_t gl, bool ipv4,
@@ -416,12 +406,12 @@ __device__ __forceinline__ void small_fetch(const BatchArgs &A,
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint32_t cr = 16u * (gl + (uint32_t)u * G);
-    it.c[u] = bld16<NT>(r, cr < eload ? lw + cr : kOOB);
+    it.c[u] = bld16(r, cr < eload ? lw + cr : kOOB, nt_step<NT>(u, U));
   }
   it.sd = load_side(sp, active ? p : A.n - 1);
 }
 
-template <int G, int U, bool NT>
+template <int G, int U, int NT>
 __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
   constexpr int GPW = 64 / G;
   const uint32_t lane = threadIdx.x & 63u;
@@ -450,8 +440,9 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
       const uint32_t hl = __shfl(ipv4_hl(it.c[0].x, it.sh), (int)(lane & ~(uint32_t)(G - 1)), 64);
       E = it.sh + (it.len < hl ? it.len : hl);
     }
-    const int E4 = (int)((E + 3u) & ~3u);
-    const int lim[4] = {E4, E4 - 4, E4 - 8, E4 - 12};
+    const int F = (int)(E & ~3u);
+    const int lim[4] = {F, F - 4, F - 8, F - 12};
+    const uint32_t tm = (1u << (8u * (E & 3u))) - 1u;
     uint32_t acc = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -459,16 +450,13 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
       if ((uint32_t)u < uf)
         acc = sum_full<false>(it.c[u], 0u, acc);
       else
-        acc = sum_masked<false>(it.c[u], cr, lim, 0u, acc);
+        acc = sum_masked<false>(it.c[u], cr, lim, tm, 0u, acc);
     }
     acc = group_total<G>(acc);
     const uint64_t p = pb + gw;
-    constexpr int LG = __builtin_ctz(G);
-    const uint32_t gbase = lane & ~(uint32_t)(G - 1);
     const Junk j = make_junk(it.sh, E, mode);
-    uint32_t jx[4];
-    junk_head_field<U, LG>(it.c, gbase, j, jx);
-    jx[1] = junk_tail<U, LG>(it.c, gbase, j, 0u);
+    uint32_t jx[3];
+    junk_take<__builtin_ctz(G)>(it.c[0], lane & ~(uint32_t)(G - 1), j, jx);
     if (gl == G - 1 && p < A.n) {
       const uint32_t v = le_to_be(acc - junk_sum<false>(jx, j, 0u), it.sh & 1u);
       finish_packet(A, p, v, it.len, it.sd,
@@ -520,7 +508,7 @@ __device__ __forceinline__ void loop_pkt(const BatchArgs &A, uint64_t p,
 }
 
 // Loads of window [wb, wb + 64*U*16) of packet k.
-template <int U, bool NT>
+template <int U, int NT>
 __device__ __forceinline__ void loop_fetch(const LoopPkt &k, uint32_t wb,
                                            uint32_t lane, uint64_t end,
                                            uint4 (&c)[U]) {
@@ -529,11 +517,11 @@ __device__ __forceinline__ void loop_fetch(const LoopPkt &k, uint32_t wb,
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint32_t cr = 16u * (lane + 64u * (uint32_t)u);
-    c[u] = bld16<NT>(r, cr < lim ? cr : kOOB);
+    c[u] = bld16(r, cr < lim ? cr : kOOB, NT != 0);
   }
 }
 
-template <int U, bool NT, bool BE>
+template <int U, int NT, bool BE>
 __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
   constexpr uint32_t W = 64u * 16u * U;
   const uint32_t lane = threadIdx.x & 63u;
@@ -551,7 +539,7 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
   LoopPkt cur, nxt;
   loop_pkt(A, p, ipv4, cur);
   Side sd = load_side(sp, p);
-  uint32_t jx[4] = {0u, 0u, 0u, 0u};  // junk dwords: head/field at window 0, tail at the last
+  uint32_t jx[3] = {0u, 0u, 0u};  // junk dwords, taken at window 0
   uint64_t pn = p + nwave;
   loop_pkt(A, pn, ipv4, nxt);
 
@@ -574,23 +562,22 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
       E = cur.sh + (l32 < hl ? l32 : hl);
     }
     const Junk j = make_junk(cur.sh, E, mode);
-    if (wb == 0) junk_head_field<U, 6>(c, 0u, j, jx);
+    if (wb == 0) junk_take<6>(c[0], 0u, j, jx);
     const uint32_t sel = (cur.sh & 1u) ? kSelIdent : kSelSwap;
-    const uint32_t E4 = (E + 3u) & ~3u;
-    if (wb + W <= E4) {  // full window (wave-uniform)
+    if (wb + W <= E) {  // full window (wave-uniform)
 #pragma unroll
       for (int u = 0; u < U; ++u) acc = sum_full<BE>(c[u], sel, acc);
     } else {
-      const int e4 = (int)(E4 - wb);
-      const int lim[4] = {e4, e4 - 4, e4 - 8, e4 - 12};
+      const int f = (int)((E & ~3u) - wb);
+      const int lim[4] = {f, f - 4, f - 8, f - 12};
+      const uint32_t tm = (1u << (8u * (E & 3u))) - 1u;
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        acc = sum_masked<BE>(c[u], 16 * (int)(lane + 64u * (uint32_t)u), lim, sel, acc);
+        acc = sum_masked<BE>(c[u], 16 * (int)(lane + 64u * (uint32_t)u), lim, tm, sel, acc);
     }
 
     if (last) {
       acc = group_total<64>(acc);
-      jx[1] = junk_tail<U, 6>(c, 0u, j, wb);
       if (lead) {
         const uint32_t s = acc - junk_sum<BE>(jx, j, sel);
         const uint32_t v = BE ? s : le_to_be(s, cur.sh & 1u);
@@ -622,12 +609,12 @@ typedef void (*KernelFn)(BatchArgs);
 struct Variant {
   const char *name;
   uint32_t window;  // bytes covered per packet step (0 = loop kernel)
-  KernelFn fn[2];   // [plain loads, non-temporal loads]
+  KernelFn fn[3];   // by load policy (bld16): plain, nt, hybrid
   uint32_t G;       // lanes per packet
 };
 
 #define YU_SMALL(G, U) \
-  {"k_small<" #G "," #U ">", 16u * G * U, {k_small<G, U, false>, k_small<G, U, true>}, G}
+  {"k_small<" #G "," #U ">", 16u * G * U, {k_small<G, U, 0>, k_small<G, U, 1>, k_small<G, U, 2>}, G}
 
 // Ordered by window; for each window the variant with the most packets per
 // wave comes first (amortises the per-packet epilogue over more bytes).
@@ -636,8 +623,8 @@ const Variant kSmall[] = {
     YU_SMALL(16, 3), YU_SMALL(16, 4), YU_SMALL(16, 6), YU_SMALL(32, 4),
     YU_SMALL(32, 6), YU_SMALL(64, 4),
 };
-const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, false, false>, k_loop<4, true, false>}, 64};
-const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, false, true>, k_loop<4, true, true>}, 64};
+const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, 0, false>, k_loop<4, 1, false>, k_loop<4, 1, false>}, 64};
+const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, 0, true>, k_loop<4, 1, true>, k_loop<4, 1, true>}, 64};
 
 // Tuning override (measurement only): YU_VARIANT=<name> forces a k_small
 // variant whenever it covers the shape.
@@ -680,7 +667,7 @@ int cu_count(int dev) {
 }
 
 // Tuning knobs (read once, measurement only). YU_BLOCKS_PER_CU: grid size in
-// 256-thread blocks per CU; YU_NT: 0 selects plain loads for packet bytes.
+// 256-thread blocks per CU; YU_NT: load policy 0/1/2 (see bld16).
 int env_int(const char *name, int lo, int hi, int dflt) {
   const char *s = getenv(name);
   if (!s || !*s) return dflt;
@@ -700,7 +687,7 @@ int blocks_per_cu(uint32_t G) {
 }
 
 int use_nt() {
-  static int v = env_int("YU_NT", 0, 1, 1);
+  static int v = env_int("YU_NT", 0, 2, 2);
   return v;
 }
 
