@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from yustack_amd import batch  # noqa: E402
+from yustack_amd.shard import max_over_ranks  # noqa: E402
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -218,10 +219,7 @@ def main():
 
     w = Workload(args.config, dev, seed=1000 + rank)
     wall, kern = timed(w, args.steps, args.warmup, dist)
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if dist:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    wall_max = float(t.item())
+    wall_max = max_over_ranks(wall, device=dev)
     ms_per_step = wall_max / args.steps * 1e3
     value = world * w.bytes * args.steps / wall_max / GIB
     achieved = w.bytes / kern / 1e9  # GB/s (decimal, like the peak)

@@ -1,0 +1,110 @@
+"""The C-ABI boundary: the library loads, exports exactly what include/yucsum.h
+declares, keeps the oracle out of the product, and fails loudly (a status, never a
+CPU fallback) when no GPU is present. CPU only — no compute calls on a device."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+from yustack_amd import _lib, batch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "yucsum.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(yu_[a-z0-9_]+)\s*\(", src)))
+
+
+def exported_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_library_loads_and_exports_header():
+    L = _lib.lib()
+    decl = declared_functions()
+    assert len(decl) >= 12
+    exported = exported_symbols()
+    for name in decl:
+        assert name in exported, name
+        assert hasattr(L, name)
+    assert set(_lib.EXPORTS) == set(decl)
+    assert L.yu_abi_version() == 1
+
+
+def test_product_does_not_link_oracle():
+    exported = exported_symbols()
+    assert not any(s.startswith("or_") for s in exported)
+    needed = subprocess.run(["readelf", "-d", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "oracle" not in needed
+    assert "libamdhip64" in needed
+
+
+def test_strerror():
+    assert _lib.strerror(0) == "ok"
+    assert _lib.strerror(-22) == "invalid argument"
+    assert _lib.strerror(-19) == "no HIP device"
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_batched_entry_points_fail_without_gpu():
+    L = _lib.lib()
+    assert L.yu_device_count() == 0
+    buf = (ctypes.c_uint8 * 64)()
+    out = (ctypes.c_uint16 * 4)()
+    rc = L.yu_csum_batch_uniform(ctypes.addressof(buf), 16, 16, 4, 0, None, 0, None, ctypes.addressof(out), None)
+    assert rc == _lib.YU_ENODEV
+    offs = (ctypes.c_uint64 * 5)(0, 16, 32, 48, 64)
+    rc = L.yu_csum_batch_ragged(ctypes.addressof(buf), ctypes.addressof(offs), 4, 0, None, 0, None,
+                                ctypes.addressof(out), None)
+    assert rc == _lib.YU_ENODEV
+    rc = L.yu_csum_batch_host_uniform(ctypes.addressof(buf), 16, 16, 4, 0, None, 0, None, ctypes.addressof(out), 0)
+    assert rc == _lib.YU_ENODEV
+
+
+def test_argument_validation_precedes_device():
+    L = _lib.lib()
+    buf = (ctypes.c_uint8 * 64)()
+    out = (ctypes.c_uint16 * 4)()
+    p, o = ctypes.addressof(buf), ctypes.addressof(out)
+    assert L.yu_csum_batch_uniform(p, 16, 16, 4, 99, None, 0, None, o, None) == _lib.YU_EINVAL  # mode
+    assert L.yu_csum_batch_uniform(p, 16, 16, 4, 0, None, 0, None, None, None) == _lib.YU_EINVAL  # out
+    assert L.yu_csum_batch_uniform(p, 16, 70000, 4, 2, None, 0, None, o, None) == _lib.YU_EINVAL  # > 65535
+    assert L.yu_csum_batch_uniform(p, 16, 4, 4, 1, None, 0, None, o, None) == _lib.YU_EINVAL  # < UDP header
+    assert L.yu_csum_batch_uniform(p, 16, 16, 0, 0, None, 0, None, o, None) == 0  # empty batch: no-op
+    assert L.yu_csum_fill_uniform(p, 16, 16, 4, 0, None, 0, None, o, None) == _lib.YU_EINVAL  # RAW not TX
+    assert L.yu_csum_fill_uniform(p + 1, 16, 16, 4, 1, None, 0, None, o, None) == _lib.YU_EINVAL  # unaligned
+    assert L.yu_csum_batch_ragged(p, None, 4, 0, None, 0, None, o, None) == _lib.YU_EINVAL
+    assert L.yu_csum_batch_host_uniform(p, 16, 16, 4, 99, None, 0, None, o, 0) == _lib.YU_EINVAL
+
+
+def test_python_front_end_refuses_cpu_tensors():
+    d = torch.zeros(64, dtype=torch.uint8)
+    with pytest.raises(TypeError):
+        batch.checksum_uniform(d, 16, 16, 4, "raw")
+    with pytest.raises(TypeError):
+        batch.checksum_ragged(d, torch.zeros(5, dtype=torch.int64), "raw")
+    with pytest.raises(ValueError):
+        batch._mode(12)
+
+
+@pytest.mark.parametrize("stride,length,mode,align,want", [
+    (64, 64, "raw", 0, "k_small<4,1>"),
+    (1500, 1500, "tcp", 0, "k_small<16,6>"),
+    (1500, 1500, "tcp", 2, "k_small<16,6>"),     # 1503 still fits 1536
+    (1536, 1536, "raw", 1, "k_small<32,4>"),     # 1539 > 1536
+    (9000, 9000, "raw", 0, "k_loop<4,LE>"),
+    (200000, 200000, "raw", 0, "k_loop<4,BE>"),  # > 131072: exact uint32 wrap path
+    (1500, 1500, "ipv4", 0, "k_small<4,1>"),     # only the <= 60-byte header is read
+    (20, 20, "udp", 3, "k_small<4,1>"),
+    (62, 62, "raw", 1, "k_small<8,1>"),      # 65 > 64
+])
+def test_variant_selection(stride, length, mode, align, want):
+    assert batch.variant(stride, length, mode, align) == want

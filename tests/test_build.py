@@ -1,0 +1,60 @@
+"""Build-level guards for the gfx950 kernels (CPU: hipcc cross-compiles here).
+
+Every kernel must keep its working set in registers: no scratch (a runtime-indexed
+register array silently becomes private memory and doubles HBM traffic —
+cdna_hip_programming.md §5.4 rule 20, hit and fixed in round 1) and no spills.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "yustack_amd", "csrc", "yucsum_kernels.hip")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.fixture(scope="module")
+def resource_usage(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("ru")
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include",
+                        "--cuda-device-only", "-c", SRC, "-o", str(out / "k.o"),
+                        "-Rpass-analysis=kernel-resource-usage"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    shutil.rmtree(out, ignore_errors=True)
+    kernels = {}
+    cur = None
+    for line in r.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            kernels[cur] = {}
+            continue
+        m = re.search(r"remark:\s+([A-Za-z \[\]/]+?): (\S+) \[", line)
+        if cur and m:
+            kernels[cur][m.group(1).strip()] = m.group(2)
+    return kernels
+
+
+def test_kernels_present(resource_usage):
+    names = " ".join(resource_usage)
+    assert "k_small" in names and "k_loop" in names
+    assert len(resource_usage) >= 20
+
+
+def test_no_scratch_no_spills(resource_usage):
+    for name, ru in resource_usage.items():
+        assert ru.get("ScratchSize [bytes/lane]") == "0", (name, ru)
+        assert ru.get("VGPRs Spill") == "0", (name, ru)
+        assert ru.get("SGPRs Spill") == "0", (name, ru)
+
+
+def test_occupancy_floor(resource_usage):
+    # at least 4 waves per SIMD everywhere: enough loads in flight per CU
+    for name, ru in resource_usage.items():
+        assert int(ru.get("Occupancy [waves/SIMD]", "0")) >= 4, (name, ru)

@@ -1,0 +1,147 @@
+"""The oracle pinned before it is trusted (CPU only).
+
+The reference is Go and cannot run here, and ships no known-answer vectors
+(SURVEY.md §8c). The oracle is pinned by RFC 1071's published example, a published
+IPv4 header checksum, the reference's own checker property on packets built like
+its test harnesses, the closed form, and agreement of two independent
+restatements (C and Python) — all recorded in tests/golden/golden.json.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "golden.json")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def _data(v):
+    if v.get("hex") is not None:
+        return bytes.fromhex(v["hex"])
+    return bytes(v["len"]) if v["kind"] == "zero" else b"\xff" * v["len"]
+
+
+def test_rfc1071_example(oracle_c):
+    d = bytes.fromhex("0001f203f4f5f6f7")
+    assert O.checksum(d, 0) == O.checksum_loop(d, 0) == oracle_c.checksum(d, 0) == 0xDDF2
+
+
+def test_published_ipv4_header():
+    d = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")
+    assert ~O.ipv4_calculate_checksum(d) & 0xFFFF == 0xB861
+    full = d[:10] + bytes.fromhex("b861") + d[12:]
+    assert O.ipv4_calculate_checksum(full) in (0, 0xFFFF)  # checker.IPv4 property
+
+
+def test_golden_raw(golden, oracle_c):
+    for v in golden["raw"]:
+        d = _data(v)
+        assert O.checksum(d, v["initial"]) == v["want"]
+        assert oracle_c.checksum(d, v["initial"]) == v["want"]
+
+
+def test_golden_wrap(golden, oracle_c):
+    for v in golden["wrap"]:
+        d = bytes([v["fill"]]) * v["len"]
+        assert oracle_c.checksum(d, v["initial"]) == v["want"]
+        assert O.checksum(d, v["initial"]) == v["want"]
+
+
+def test_golden_pseudo(golden, oracle_c):
+    for v in golden["pseudo"]:
+        s, d = bytes.fromhex(v["src"]), bytes.fromhex(v["dst"])
+        assert O.pseudo_header_checksum(v["proto"], s, d) == v["want"]
+        assert oracle_c.pseudo_header_checksum(v["proto"], s, d) == v["want"]
+
+
+def test_golden_harness_packets_pass_checker(golden):
+    """checker.IPv4 / checker.TCP semantics on packets built like the reference's
+    test harnesses (checker/checker.go:32-35,80-92)."""
+    for h in golden["harness"]:
+        pk = bytes.fromhex(h["hex"])
+        assert O.ipv4_calculate_checksum(pk) in (0, 0xFFFF)
+        mode = O.MODE_VERIFY_TCP if h["proto"] == "tcp" else O.MODE_VERIFY_UDP
+        assert O.packet(mode, pk[20:], addrs=pk[12:20]) in (0, 0xFFFF)
+        # and the stored field equals the TX composition over the same bytes
+        txm = O.MODE_TCP if h["proto"] == "tcp" else O.MODE_UDP
+        assert O.packet(txm, pk[20:], addrs=pk[12:20]) == h["transport_field"]
+        assert O.packet(O.MODE_IPV4, pk) == h["ipv4_field"]
+
+
+def test_golden_batch_modes(golden, oracle_c):
+    b = golden["batch"]
+    blob = np.frombuffer(bytes.fromhex(b["hex"]), np.uint8)
+    offs = np.array(b["offsets"], np.uint64)
+    addrs = np.frombuffer(bytes.fromhex(b["addrs"]), np.uint8)
+    init = np.array(b["initial"], np.uint16)
+    for name, want in b["modes"].items():
+        m = {v: k for k, v in O.MODE_NAMES.items()}[name]
+        got_a = oracle_c.batch(blob, m, offsets=offs, addrs=addrs if m in (1, 2, 6, 7) else None)
+        got_i = oracle_c.batch(blob, m, offsets=offs, initial_arr=init)
+        assert got_a.tolist() == want["with_addrs"], name
+        assert got_i.tolist() == want["with_initial"], name
+
+
+def test_twins_agree_random(oracle_c):
+    rng = random.Random(99)
+    for _ in range(400):
+        n = rng.choice([0, 1, 2, 3, 5, 64, 65, 1500, 1501, rng.randint(0, 4000)])
+        d = bytes(rng.getrandbits(8) for _ in range(n))
+        init = rng.getrandbits(16)
+        a = O.checksum_loop(d, init)
+        assert a == O.checksum(d, init) == oracle_c.checksum(d, init) == O.checksum_closed_form(d, init)
+
+
+def test_closed_form_zero_vs_ffff():
+    # 0x0000 only for all-zero input with initial 0; any other multiple of 65535 -> 0xFFFF
+    assert O.checksum(bytes(10), 0) == 0
+    assert O.checksum(b"\xff\xff", 0) == 0xFFFF
+    assert O.checksum(bytes(10), 0xFFFF) == 0xFFFF
+    assert O.checksum(b"\x80\x00\x7f\xff", 0) == 0xFFFF
+
+
+@pytest.mark.parametrize("mode", list(range(8)))
+def test_c_vs_python_compositions(oracle_c, mode):
+    rng = np.random.default_rng(mode)
+    lo = {1: 8, 2: 60, 4: 4, 3: 60, 5: 60, 6: 60}.get(mode, 0)
+    lens = rng.integers(lo, 300, size=40)
+    offs = np.zeros(41, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    blob = rng.integers(0, 256, size=int(offs[-1]), dtype=np.uint8)
+    for p in range(40):
+        s = int(offs[p])
+        if mode in (2, 6):
+            blob[s + 12] = int(rng.integers(5, 16)) << 4
+        if mode in (3, 5):
+            blob[s] = 0x40 | int(rng.integers(0, 16))
+    addrs = rng.integers(0, 256, size=320, dtype=np.uint8)
+    init = rng.integers(0, 65536, size=40, dtype=np.uint16)
+    for kw in ({"addrs": addrs}, {"initial_arr": init}, {"initial": 0xBEEF}):
+        want = O.batch_ragged_py(blob.tobytes(), offs, mode, **kw)
+        got = oracle_c.batch(blob, mode, offsets=offs, **kw)
+        assert (got == want).all(), (mode, list(kw))
+        # uniform layout agrees with ragged on equal-length packets
+    L = 80 if mode not in (2, 6) else 80
+    ublob = rng.integers(0, 256, size=L * 16, dtype=np.uint8)
+    ublob[12::L] = 0x50
+    ublob[0::L] = 0x45
+    u = oracle_c.batch(ublob, mode, stride=L, length=L, n=16, initial_arr=init[:16])
+    r = oracle_c.batch(ublob, mode, offsets=np.arange(17, dtype=np.uint64) * L, initial_arr=init[:16])
+    assert (u == r).all()
+
+
+def test_oracle_multithreaded_matches_single(oracle_c):
+    rng = np.random.default_rng(3)
+    blob = rng.integers(0, 256, size=1500 * 1000, dtype=np.uint8)
+    a = oracle_c.batch(blob, O.MODE_RAW, stride=1500, length=1500, n=1000, threads=1)
+    b = oracle_c.batch(blob, O.MODE_RAW, stride=1500, length=1500, n=1000, threads=7)
+    assert (a == b).all()
