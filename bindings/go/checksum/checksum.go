@@ -1,0 +1,120 @@
+// Package checksum is a drop-in replacement for yustack's package checksum
+// (github.com/YaoZengzeng/yustack/checksum, reference checksum/checksum.go).
+//
+// The three package functions keep their exact signatures, so header/ipv4.go,
+// header/tcp.go, header/udp.go, types/route.go, transport/udp/endpoint.go,
+// transport/tcp/connect.go, network/ipv4/icmp.go and checker/checker.go build
+// unchanged. They bind the scalar entry points of the C ABI (include/yucsum.h,
+// libyucsum.so). Batches go to the GPU through BatchHostUniform.
+//
+// Status: written against the C ABI; not compiled in the build container (it
+// has no Go toolchain). See INTEGRATION.md for how to build and swap it in.
+package checksum
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../../yustack_amd -lyucsum -Wl,-rpath,${SRCDIR}/../../../yustack_amd
+#include <stdlib.h>
+#include "yucsum.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"unsafe"
+)
+
+// cgoMin is the buffer length below which the sum stays in Go: a cgo call
+// costs ~100 ns, more than summing a 20-byte header.
+const cgoMin = 256
+
+// Checksum calculates the checksum of the bytes in the given byte array
+// (reference checksum/checksum.go:4-18). Not complemented.
+func Checksum(buf []byte, initial uint16) uint16 {
+	if len(buf) < cgoMin {
+		return goSum(buf, initial)
+	}
+	return uint16(C.yu_checksum((*C.uint8_t)(unsafe.Pointer(&buf[0])), C.size_t(len(buf)),
+		C.uint16_t(initial)))
+}
+
+// goSum: the same uint32 accumulation (wrap included) for short buffers.
+func goSum(buf []byte, initial uint16) uint16 {
+	v := uint32(initial)
+	n := len(buf)
+	if n&1 != 0 {
+		n--
+		v += uint32(buf[n]) << 8
+	}
+	for i := 0; i < n; i += 2 {
+		v += uint32(buf[i])<<8 | uint32(buf[i+1])
+	}
+	return ChecksumCombine(uint16(v), uint16(v>>16))
+}
+
+// PseudoHeaderChecksum calculates the pseudo header checksum for the given
+// destination protocol and network addresses, ignoring the length field
+// (reference checksum/checksum.go:24-28).
+func PseudoHeaderChecksum(protocol uint32, srcAddr string, dstAddr string) uint16 {
+	xsum := Checksum([]byte(srcAddr), 0)
+	xsum = Checksum([]byte(dstAddr), xsum)
+	return Checksum([]byte{0, uint8(protocol)}, xsum)
+}
+
+// ChecksumCombine combines the two uint16 to form their checksum
+// (reference checksum/checksum.go:32-35).
+func ChecksumCombine(a, b uint16) uint16 {
+	v := uint32(a) + uint32(b)
+	return uint16(v + v>>16)
+}
+
+// Mode selects the reference composition a batch reproduces (include/yucsum.h).
+type Mode int
+
+const (
+	ModeRaw        Mode = C.YU_MODE_RAW
+	ModeUDP        Mode = C.YU_MODE_UDP
+	ModeTCP        Mode = C.YU_MODE_TCP
+	ModeIPv4       Mode = C.YU_MODE_IPV4
+	ModeICMP       Mode = C.YU_MODE_ICMP
+	ModeVerifyIPv4 Mode = C.YU_MODE_VERIFY_IPV4
+	ModeVerifyTCP  Mode = C.YU_MODE_VERIFY_TCP
+	ModeVerifyUDP  Mode = C.YU_MODE_VERIFY_UDP
+)
+
+// ErrNoDevice is returned when no MI355X (HIP device) is usable.
+var ErrNoDevice = errors.New("checksum: no HIP device")
+
+// BatchHostUniform computes one result per packet of a uniform-stride batch in
+// host memory (packet i = data[i*stride : i*stride+length]) on GPU `device`.
+// initial (len n) and addrs (len 8n, {src[4], dst[4]}) are optional. The C
+// side copies into its own pinned staging and retains no Go pointer.
+func BatchHostUniform(data []byte, stride uint64, length uint32, n uint64, mode Mode,
+	initial []uint16, addrs []byte, out []uint16, device int) error {
+	if n == 0 {
+		return nil
+	}
+	if uint64(len(out)) < n || uint64(len(data)) < (n-1)*stride+uint64(length) {
+		return fmt.Errorf("checksum: batch buffers too small")
+	}
+	var pi *C.uint16_t
+	if initial != nil {
+		pi = (*C.uint16_t)(unsafe.Pointer(&initial[0]))
+	}
+	var pa *C.uint8_t
+	if addrs != nil {
+		pa = (*C.uint8_t)(unsafe.Pointer(&addrs[0]))
+	}
+	rc := C.yu_csum_batch_host_uniform((*C.uint8_t)(unsafe.Pointer(&data[0])), C.uint64_t(stride),
+		C.uint32_t(length), C.uint64_t(n), C.int(mode), pi, 0, pa,
+		(*C.uint16_t)(unsafe.Pointer(&out[0])), C.int(device))
+	switch {
+	case rc == C.YU_OK:
+		return nil
+	case rc == C.YU_ENODEV:
+		return ErrNoDevice
+	default:
+		return fmt.Errorf("checksum: %s (%d)", C.GoString(C.yu_strerror(rc)), int(rc))
+	}
+}

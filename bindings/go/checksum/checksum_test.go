@@ -1,0 +1,54 @@
+package checksum
+
+import (
+	"math/rand"
+	"testing"
+)
+
+// refChecksum is the reference loop (checksum/checksum.go:4-18) restated for
+// comparison; it is test-only.
+func refChecksum(buf []byte, initial uint16) uint16 {
+	v := uint32(initial)
+	l := len(buf)
+	if l&1 != 0 {
+		l--
+		v += uint32(buf[l]) << 8
+	}
+	for i := 0; i < l; i += 2 {
+		v += (uint32(buf[i]) << 8) + uint32(buf[i+1])
+	}
+	return ChecksumCombine(uint16(v), uint16(v>>16))
+}
+
+func TestRFC1071(t *testing.T) {
+	if got := Checksum([]byte{0x00, 0x01, 0xf2, 0x03, 0xf4, 0xf5, 0xf6, 0xf7}, 0); got != 0xddf2 {
+		t.Fatalf("got 0x%x want 0xddf2", got)
+	}
+}
+
+func TestAgainstReferenceLoop(t *testing.T) {
+	r := rand.New(rand.NewSource(1))
+	for i := 0; i < 2000; i++ {
+		b := make([]byte, r.Intn(5000))
+		r.Read(b)
+		init := uint16(r.Intn(65536))
+		if Checksum(b, init) != refChecksum(b, init) {
+			t.Fatalf("len %d", len(b))
+		}
+	}
+	ff := make([]byte, 131074)
+	for i := range ff {
+		ff[i] = 0xff
+	}
+	if Checksum(ff, 0xffff) != 65534 {
+		t.Fatal("uint32 wrap")
+	}
+}
+
+func BenchmarkChecksum1500(b *testing.B) {
+	buf := make([]byte, 1500)
+	b.SetBytes(1500)
+	for i := 0; i < b.N; i++ {
+		Checksum(buf, 0)
+	}
+}

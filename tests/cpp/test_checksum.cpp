@@ -1,0 +1,232 @@
+// C++ parity tests over include/yustack/checksum.hpp (the host-side mirror of
+// the reference API) — written the way the reference's Go tests are:
+// packets are built like transport/tcp/testing/context/context.go:164-209
+// (SendPacket) and transport/udp/udp_test.go:105-144 (sendPacket) and every
+// packet must pass checker.IPv4 / checker.TCP (checker/checker.go:25-99).
+// The CPU part also compares the scalar path with the C oracle (test
+// infrastructure, linked only here). `--gpu` runs the batched device path on
+// the same packets.
+//
+// usage: test_checksum [--gpu]
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <random>
+#include <string>
+#include <vector>
+
+#include "yustack/checksum.hpp"
+
+extern "C" {
+uint16_t or_checksum(const uint8_t *buf, size_t len, uint16_t initial);
+uint16_t or_packet(int mode, const uint8_t *pkt, uint64_t len, const uint16_t *initial_arr,
+                   uint16_t initial, const uint8_t *addrs, uint64_t p);
+}
+
+using namespace yustack;
+
+static int g_fail = 0;
+#define EXPECT(cond, ...)                                          \
+  do {                                                             \
+    if (!(cond)) {                                                 \
+      fprintf(stderr, "FAIL %s:%d: %s: ", __FILE__, __LINE__, #cond); \
+      fprintf(stderr, __VA_ARGS__);                                \
+      fprintf(stderr, "\n");                                       \
+      ++g_fail;                                                    \
+    }                                                              \
+  } while (0)
+
+static const std::string kStackAddr = std::string("\x0a\x00\x00\x01", 4);  // context.go:23
+static const std::string kTestAddr = std::string("\x0a\x00\x00\x02", 4);   // context.go:30
+
+// context.go:164-209 — Context.SendPacket
+static std::vector<uint8_t> tcp_packet(const std::vector<uint8_t> &payload, uint16_t srcPort,
+                                       uint16_t dstPort, uint32_t seq, uint32_t ack, uint8_t flags,
+                                       uint16_t rcvWnd, const std::vector<uint8_t> &opts = {}) {
+  std::vector<uint8_t> buf(header::TCPMinimumSize + header::IPv4MinimumSize + opts.size() +
+                           payload.size());
+  memcpy(buf.data() + buf.size() - payload.size(), payload.data(), payload.size());
+  memcpy(buf.data() + buf.size() - payload.size() - opts.size(), opts.data(), opts.size());
+  header::IPv4 ip{buf.data()};
+  ip.Encode(header::IPv4MinimumSize, (uint16_t)buf.size(), 6, kTestAddr, kStackAddr);
+  ip.SetChecksum((uint16_t)~ip.CalculateChecksum());
+  header::TCP t{buf.data() + header::IPv4MinimumSize};
+  t.Encode(srcPort, dstPort, seq, ack, (uint8_t)(header::TCPMinimumSize + opts.size()), flags,
+           rcvWnd);
+  uint16_t xsum = checksum::Checksum(kTestAddr, 0);
+  xsum = checksum::Checksum(kStackAddr, xsum);
+  const uint8_t proto[2] = {0, 6};
+  xsum = checksum::Checksum(proto, 2, xsum);
+  const uint16_t length = (uint16_t)(header::TCPMinimumSize + opts.size() + payload.size());
+  xsum = checksum::Checksum(payload, xsum);
+  t.SetChecksum((uint16_t)~t.CalculateChecksum(xsum, length));
+  return buf;
+}
+
+// udp_test.go:105-144 — testContext.sendPacket (addresses udp_test.go:21-25)
+static std::vector<uint8_t> udp_packet(const std::vector<uint8_t> &payload, uint16_t srcPort,
+                                       uint16_t dstPort) {
+  const std::string testAddr("\x0a\x01\x00\x01", 4), stackAddr("\x0a\x01\x00\x02", 4);
+  std::vector<uint8_t> buf(header::UDPMinimumSize + header::IPv4MinimumSize + payload.size());
+  memcpy(buf.data() + buf.size() - payload.size(), payload.data(), payload.size());
+  header::IPv4 ip{buf.data()};
+  ip.Encode(header::IPv4MinimumSize, (uint16_t)buf.size(), 17, testAddr, stackAddr);
+  ip.SetChecksum((uint16_t)~ip.CalculateChecksum());
+  header::UDP u{buf.data() + header::IPv4MinimumSize};
+  u.Encode(srcPort, dstPort, (uint16_t)(header::UDPMinimumSize + payload.size()));
+  uint16_t xsum = checksum::Checksum(testAddr, 0);
+  xsum = checksum::Checksum(stackAddr, xsum);
+  const uint8_t proto[2] = {0, 17};
+  xsum = checksum::Checksum(proto, 2, xsum);
+  const uint16_t length = (uint16_t)(header::UDPMinimumSize + payload.size());
+  xsum = checksum::Checksum(payload, xsum);
+  u.SetChecksum((uint16_t)~u.CalculateChecksum(xsum, length));
+  return buf;
+}
+
+static std::vector<uint8_t> rand_bytes(std::mt19937 &rng, size_t n) {
+  std::vector<uint8_t> v(n);
+  for (auto &b : v) b = (uint8_t)rng();
+  return v;
+}
+
+static void test_known_answers() {
+  const uint8_t rfc[8] = {0x00, 0x01, 0xf2, 0x03, 0xf4, 0xf5, 0xf6, 0xf7};
+  EXPECT(checksum::Checksum(rfc, 8, 0) == 0xddf2, "RFC 1071 example");
+  std::vector<uint8_t> ff(131074, 0xff);
+  EXPECT(checksum::Checksum(ff, 0xffff) == 65534, "uint32 wrap");
+  EXPECT(checksum::ChecksumCombine(0xffff, 0xffff) == 0xffff, "combine");
+}
+
+static void test_scalar_vs_oracle() {
+  std::mt19937 rng(7);
+  for (int i = 0; i < 3000; ++i) {
+    const size_t n = (i % 7 == 0) ? 131072 + rng() % 5 : rng() % 4000;
+    auto d = rand_bytes(rng, n);
+    const uint16_t init = (uint16_t)rng();
+    EXPECT(checksum::Checksum(d, init) == or_checksum(d.data(), d.size(), init), "n=%zu", n);
+  }
+}
+
+// tcp_test.go: data payloads {1,2,3} (:145,524,731), SYN options (MSS + WS)
+static std::vector<std::vector<uint8_t>> harness_packets(std::mt19937 &rng, int count) {
+  std::vector<std::vector<uint8_t>> v;
+  v.push_back(tcp_packet({1, 2, 3}, 4096, 1234, 790, 1000, 0x18, 30000));
+  v.push_back(tcp_packet({}, 4096, 1234, 789, 0, 0x02, 30000, {2, 4, 5, 180, 1, 3, 3, 7}));
+  while ((int)v.size() < count) {
+    auto payload = rand_bytes(rng, rng() % 1461);
+    v.push_back(tcp_packet(payload, 4096, 1234, rng(), rng(), 0x18, (uint16_t)rng()));
+  }
+  return v;
+}
+
+static void test_harness_packets_pass_checker() {
+  std::mt19937 rng(11);
+  for (auto &pk : harness_packets(rng, 200)) {
+    EXPECT(checker::IPv4(pk.data(), pk.size()), "checker.IPv4");
+    EXPECT(checker::TCP(pk.data(), pk.size()), "checker.TCP");
+    // the stored field is what the oracle's sendTCP composition predicts
+    header::TCP t{pk.data() + 20};
+    EXPECT(t.Checksum() == or_packet(2, pk.data() + 20, pk.size() - 20, nullptr, 0, pk.data() + 12, 0),
+           "tcp field");
+  }
+  for (int i = 0; i < 200; ++i) {
+    auto payload = rand_bytes(rng, 30 + rng() % 100);  // udp_test.go:97-103
+    auto pk = udp_packet(payload, 4096, 1234);
+    EXPECT(checker::IPv4(pk.data(), pk.size()), "udp checker.IPv4");
+    header::UDP u{pk.data() + 20};
+    EXPECT(u.Checksum() == or_packet(1, pk.data() + 20, pk.size() - 20, nullptr, 0, pk.data() + 12, 0),
+           "udp field");
+  }
+  auto pk = tcp_packet({1, 2, 3}, 4096, 1234, 790, 1000, 0x18, 30000);
+  pk[41] ^= 0x40;
+  EXPECT(!checker::TCP(pk.data(), pk.size()), "corrupted packet must fail");
+}
+
+#define HIPCK(x)                                                            \
+  do {                                                                      \
+    hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess) {                                                 \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(2);                                                              \
+    }                                                                       \
+  } while (0)
+
+// The batched GPU path on the same packets: RX verification of whole IPv4
+// packets (checker semantics) and TX field values of the TCP segments.
+static void test_gpu_batches() {
+  std::mt19937 rng(23);
+  auto pks = harness_packets(rng, 4096);
+  std::vector<uint8_t> blob, segs, addrs;
+  std::vector<uint64_t> off{0}, soff{0};
+  std::vector<uint16_t> fields;
+  for (auto &pk : pks) {
+    blob.insert(blob.end(), pk.begin(), pk.end());
+    off.push_back(blob.size());
+    segs.insert(segs.end(), pk.begin() + 20, pk.end());
+    soff.push_back(segs.size());
+    addrs.insert(addrs.end(), pk.begin() + 12, pk.begin() + 20);
+    fields.push_back(header::TCP{pk.data() + 20}.Checksum());
+  }
+  const uint64_t n = pks.size();
+  uint8_t *d_blob, *d_segs, *d_addrs;
+  uint64_t *d_off, *d_soff;
+  uint16_t *d_out;
+  HIPCK(hipMalloc(&d_blob, blob.size()));
+  HIPCK(hipMalloc(&d_segs, segs.size()));
+  HIPCK(hipMalloc(&d_addrs, addrs.size()));
+  HIPCK(hipMalloc(&d_off, off.size() * 8));
+  HIPCK(hipMalloc(&d_soff, soff.size() * 8));
+  HIPCK(hipMalloc(&d_out, n * 2));
+  HIPCK(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(d_segs, segs.data(), segs.size(), hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(d_addrs, addrs.data(), addrs.size(), hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(d_soff, soff.data(), soff.size() * 8, hipMemcpyHostToDevice));
+  std::vector<uint16_t> out(n);
+  batch::Side side;
+  side.addrs = d_addrs;
+
+  batch::Ragged(d_blob, d_off, n, batch::VERIFY_IPV4, d_out);
+  HIPCK(hipMemcpy(out.data(), d_out, n * 2, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < n; ++i) EXPECT(out[i] == 0 || out[i] == 0xffff, "verify_ipv4 %lu", i);
+
+  batch::Ragged(d_segs, d_soff, n, batch::VERIFY_TCP, d_out, side);
+  HIPCK(hipMemcpy(out.data(), d_out, n * 2, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < n; ++i) EXPECT(out[i] == 0 || out[i] == 0xffff, "verify_tcp %lu", i);
+
+  batch::Ragged(d_segs, d_soff, n, batch::TCP, d_out, side);  // TX: field taken as 0
+  HIPCK(hipMemcpy(out.data(), d_out, n * 2, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < n; ++i) EXPECT(out[i] == fields[i], "tcp field %lu", i);
+
+  bool threw = false;
+  try {
+    batch::Uniform(d_segs, 16, 70000, 1, batch::TCP, d_out);
+  } catch (const Error &e) {
+    threw = e.status() == YU_EINVAL;
+  }
+  EXPECT(threw, "oversize transport packet must throw EINVAL");
+  HIPCK(hipFree(d_blob));
+  HIPCK(hipFree(d_segs));
+  HIPCK(hipFree(d_addrs));
+  HIPCK(hipFree(d_off));
+  HIPCK(hipFree(d_soff));
+  HIPCK(hipFree(d_out));
+}
+
+int main(int argc, char **argv) {
+  const bool gpu = argc > 1 && strcmp(argv[1], "--gpu") == 0;
+  test_known_answers();
+  test_scalar_vs_oracle();
+  test_harness_packets_pass_checker();
+  if (gpu) test_gpu_batches();
+  if (g_fail) {
+    fprintf(stderr, "%d failure(s)\n", g_fail);
+    return 1;
+  }
+  printf("ok%s\n", gpu ? " (cpu+gpu)" : " (cpu)");
+  return 0;
+}

@@ -96,7 +96,9 @@ def test_python_front_end_refuses_cpu_tensors():
 
 
 @pytest.mark.parametrize("stride,length,mode,align,want", [
-    (64, 64, "raw", 0, "k_small<4,1>"),
+    (64, 64, "raw", 0, "k_tiny<4>"),
+    (64, 64, "udp", 0, "k_small<4,1>"),      # TX field: junk -> k_small
+    (128, 120, "verify_tcp", 0, "k_tiny<8>"),
     (1500, 1500, "tcp", 0, "k_small<16,6>"),
     (1500, 1500, "tcp", 2, "k_small<16,6>"),     # 1503 still fits 1536
     (1536, 1536, "raw", 1, "k_small<32,4>"),     # 1539 > 1536

@@ -469,6 +469,90 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
 }
 
 // ---------------------------------------------------------------------
+// k_tiny<G, NT>: uniform stride, packets of <= 16G bytes starting 4-byte
+// aligned, in the modes without junk bytes (RAW, VERIFY_TCP, VERIFY_UDP).
+// For tiny packets k_small spends a whole per-packet epilogue on every 1 KiB
+// loaded; here a wave step covers 64 packets (G KiB): group g (G lanes) loads
+// chunk j of G packets (slot k holds packet pb + (64/G)k + g, so each load
+// instruction reads 64/G consecutive packets = one contiguous KiB). After the
+// per-slot group sums, a cross-lane transpose gives slot j's total to lane j
+// of the group, and all 64 lanes finish one packet each.
+// ---------------------------------------------------------------------
+template <int G>
+struct TinyItem {
+  uint4 c[G];
+  Side sd;  // side data of the packet this lane finishes
+};
+
+template <int G, int NT>
+__device__ __forceinline__ void tiny_fetch(const BatchArgs &A, const SidePtrs &sp,
+                                           uint64_t pb, uint32_t g, uint32_t j,
+                                           TinyItem<G> &it) {
+  constexpr uint32_t GPW = 64 / G;
+  const uint64_t base = uniform64((uint64_t)(uintptr_t)A.data + pb * A.stride);
+  const __amdgpu_buffer_rsrc_t r = rsrc_at(base, A.end);
+  const bool in = 16u * j < A.len;
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    const uint32_t q = GPW * (uint32_t)k + g;  // packet pb + q
+    const bool active = in && pb + q < A.n;
+    it.c[k] = bld16(r, active ? (uint32_t)(q * A.stride) + 16u * j : kOOB, NT != 0);
+  }
+  const uint64_t pf = pb + GPW * j + g;
+  it.sd = load_side(sp, pf < A.n ? pf : A.n - 1);
+}
+
+// Every lane of each G-lane group gets the value of the group's last lane.
+template <int G>
+__device__ __forceinline__ uint32_t bcast_last(uint32_t v, uint32_t lane) {
+  if (G == 4)  // quad_perm [3,3,3,3]
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xFF, 0xf, 0xf, false);
+  return (uint32_t)__shfl(v, (int)(lane | (G - 1)), 64);
+}
+
+template <int G, int NT>
+__global__ __launch_bounds__(256) void k_tiny(BatchArgs A) {
+  constexpr uint32_t GPW = 64 / G;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t j = lane & (G - 1);
+  const uint32_t g = lane / G;
+  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                        (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t step = (uint64_t)gridDim.x * (blockDim.x >> 6) * 64u;
+  const SidePtrs sp = side_ptrs(A);
+  const uint32_t E = A.len;  // window base = packet start (4-aligned)
+  const int F = (int)(E & ~3u);
+  const int lim[4] = {F, F - 4, F - 8, F - 12};
+  const uint32_t tm = (1u << (8u * (E & 3u))) - 1u;
+  const bool full = A.uf != 0;  // every chunk of every packet is whole
+
+  uint64_t pb = wave * 64u;
+  if (pb >= A.n) return;
+  TinyItem<G> it;
+  tiny_fetch<G, NT>(A, sp, pb, g, j, it);
+  for (;;) {
+    const uint64_t pn = pb + step;
+    const bool more = pn < A.n;  // wave-uniform
+    TinyItem<G> nx;
+    tiny_fetch<G, NT>(A, sp, more ? pn : A.n, g, j, nx);
+
+    uint32_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      uint32_t acc = full ? sum_full<false>(it.c[k], 0u, 0u)
+                          : sum_masked<false>(it.c[k], 16 * (int)j, lim, tm, 0u, 0u);
+      acc = bcast_last<G>(group_total<G>(acc), lane);
+      mine = (j == (uint32_t)k) ? acc : mine;
+    }
+    const uint64_t pf = pb + GPW * j + g;
+    if (pf < A.n) finish_packet(A, pf, le_to_be(mine, 0u), E, it.sd, nullptr, E);
+    if (!more) break;
+    it = nx;
+    pb = pn;
+  }
+}
+
+// ---------------------------------------------------------------------
 // k_loop<U, NT, BE>: one wave per packet, 64*U*16-byte windows (ragged /
 // large packets). The wave walks a stream of (packet, window) items and
 // always issues the loads of the next item — the next window of this
@@ -611,10 +695,15 @@ struct Variant {
   uint32_t window;  // bytes covered per packet step (0 = loop kernel)
   KernelFn fn[3];   // by load policy (bld16): plain, nt, hybrid
   uint32_t G;       // lanes per packet
+  uint32_t ppw;     // packets per wave step
 };
 
 #define YU_SMALL(G, U) \
-  {"k_small<" #G "," #U ">", 16u * G * U, {k_small<G, U, 0>, k_small<G, U, 1>, k_small<G, U, 2>}, G}
+  {"k_small<" #G "," #U ">", 16u * G * U, {k_small<G, U, 0>, k_small<G, U, 1>, k_small<G, U, 2>}, G, 64u / G}
+#define YU_TINY(G) \
+  {"k_tiny<" #G ">", 16u * G, {k_tiny<G, 0>, k_tiny<G, 1>, k_tiny<G, 1>}, G, 64u}
+
+const Variant kTiny[] = {YU_TINY(4), YU_TINY(8)};
 
 // Ordered by window; for each window the variant with the most packets per
 // wave comes first (amortises the per-packet epilogue over more bytes).
@@ -623,8 +712,8 @@ const Variant kSmall[] = {
     YU_SMALL(16, 3), YU_SMALL(16, 4), YU_SMALL(16, 6), YU_SMALL(32, 4),
     YU_SMALL(32, 6), YU_SMALL(64, 4),
 };
-const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, 0, false>, k_loop<4, 1, false>, k_loop<4, 1, false>}, 64};
-const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, 0, true>, k_loop<4, 1, true>, k_loop<4, 1, true>}, 64};
+const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, 0, false>, k_loop<4, 1, false>, k_loop<4, 1, false>}, 64, 1};
+const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, 0, true>, k_loop<4, 1, true>, k_loop<4, 1, true>}, 64, 1};
 
 // Tuning override (measurement only): YU_VARIANT=<name> forces a k_small
 // variant whenever it covers the shape.
@@ -641,16 +730,26 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
   const uint64_t span = need + (aligned4 ? 0 : 3);
   // lane window offsets are 32-bit: (64/G - 1) strides + the window
   auto fits = [&](const Variant &v) {
-    return span <= v.window && (64u / v.G) * stride + v.window < kOOB;
+    return span <= v.window && v.ppw * stride + v.window < kOOB;
   };
+  // k_tiny: no junk bytes (4-aligned starts, no TX field, no IPv4 header walk)
+  const bool tiny_ok = aligned4 && (mode == YU_MODE_RAW || mode == YU_MODE_VERIFY_TCP ||
+                                    mode == YU_MODE_VERIFY_UDP);
   if (const char *f = forced_variant()) {
     for (const Variant &v : kSmall)
       if (strcmp(v.name, f) == 0 && fits(v)) return v;
+    for (const Variant &v : kTiny)
+      if (strcmp(v.name, f) == 0 && tiny_ok && fits(v)) return v;
   }
+  if (tiny_ok)
+    for (const Variant &v : kTiny)
+      if (fits(v)) return v;
   for (const Variant &v : kSmall)
     if (fits(v)) return v;
   return len > kLEMax ? kLoopBE : kLoopLE;
 }
+
+bool is_tiny(const Variant &v) { return v.ppw == 64u && v.G < 64u; }
 
 std::atomic<int> g_cu_count[64];
 
@@ -703,7 +802,7 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_status(e);
   const uint64_t waves_per_block = 4;
-  const uint64_t ppw = 64u / v.G;
+  const uint64_t ppw = v.ppw;
   uint64_t waves = (A.n + ppw - 1) / ppw;
   uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
   uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu(v.G);
@@ -756,7 +855,10 @@ int batch_uniform(const uint8_t *data, uint8_t *fill, uint64_t stride,
   A.initial = initial;
   A.mode = mode;
   const Variant &v = pick_uniform((uintptr_t)data, stride, len, n, mode);
-  A.uf = v.window ? (mode_is_ipv4(mode) ? 0u : len / (16u * v.G)) : 0u;
+  if (is_tiny(v))
+    A.uf = len >= 16u * v.G ? 1u : 0u;  // k_tiny: all chunks whole?
+  else
+    A.uf = v.window ? (mode_is_ipv4(mode) ? 0u : len / (16u * v.G)) : 0u;
   return launch(v, A, (hipStream_t)stream);
 }
 
