@@ -188,6 +188,36 @@ def cpu_baseline(w: Workload, threads: int, budget_s: float):
     }
 
 
+def end_to_end(w: Workload, reps: int = 3):
+    """Host memory in, host results out (yu_csum_batch_host_uniform: pinned
+    staging, H2D / kernel / D2H pipelined over 3 streams), config 3 shape. Reported
+    in DESIGN.md, never as `value`. Pageable = numpy buffer (CPU memcpy into the
+    library's pinned slots); pinned = page-locked torch tensor (DMA straight from it)."""
+    if w.offsets is not None:
+        return None
+    host = w.data[0].cpu().numpy()
+    addrs = None if w.addrs is None else w.addrs.cpu().numpy()
+    init = None if w.initial_arr is None else w.initial_arr.cpu().numpy()
+    pinned = torch.from_numpy(host).pin_memory()
+    out = np.empty(w.n, np.uint16)
+    res = {}
+    for kind, src in (("pageable", host), ("pinned", pinned)):
+        batch.checksum_host_uniform(src, w.L, w.L, w.n, w.mode, initial_arr=init, addrs=addrs, out=out,
+                                    device=w.dev.index or 0)  # warm-up: staging allocation
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            batch.checksum_host_uniform(src, w.L, w.L, w.n, w.mode, initial_arr=init, addrs=addrs,
+                                        out=out, device=w.dev.index or 0)
+        dt = (time.perf_counter() - t0) / reps
+        res[f"{kind}_GiB_s"] = round(w.bytes / dt / GIB, 2)
+        res[f"{kind}_ms"] = round(dt * 1e3, 2)
+    w.step(0)
+    torch.cuda.synchronize()
+    res["matches_device_path"] = bool(np.array_equal(out, w.out.cpu().numpy()))
+    res["bytes"] = w.bytes
+    return res
+
+
 def host_threads() -> int:
     try:
         n = len(os.sched_getaffinity(0))
@@ -205,6 +235,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip configs 2/4 side measurements")
     ap.add_argument("--cpu-budget", type=float, default=6.0, help="wall seconds for the CPU baseline")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -289,6 +320,9 @@ def main():
             del wc
             torch.cuda.empty_cache()
         res["other_configs"] = extra
+
+    if rank == 0 and world == 1 and not args.no_e2e:
+        res["end_to_end_host_memory"] = end_to_end(w)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         parity, cb = cpu_baseline(w, host_threads(), args.cpu_budget)

@@ -15,35 +15,54 @@ import os
 import statistics
 import sys
 
-KERNELS = {"config2": "k_small<4, 1, true>", "config3": "k_small<16, 6, true>",
-           "config4": "k_loop<4, true, true>"}
-NAMES = {"k_small<4, 1, true>": "k_small<4,1>", "k_small<16, 6, true>": "k_small<16,6>",
-         "k_loop<4, true, true>": "k_loop<4,BE>"}
+import re
 
 
-def per_launch(path, kernel):
-    vals = []
+def short_name(full):
+    """'void (anonymous namespace)::k_small<16, 6, 2>(...)' -> 'k_small<16,6>' (the
+    name bench.py reports; the load-policy template argument is dropped)."""
+    m = re.search(r"::(k_\w+)<([^>]*)>", full)
+    if not m:
+        return None
+    k, args = m.group(1), [a.strip() for a in m.group(2).split(",")]
+    if k == "k_small":
+        return f"k_small<{args[0]},{args[1]}>"
+    if k == "k_tiny":
+        return f"k_tiny<{args[0]}>"
+    if k == "k_loop":
+        return f"k_loop<{args[0]},{'BE' if args[2] == 'true' else 'LE'}>"
+    return k
+
+
+def per_launch(path):
+    """Median counter value per launch of the checksum kernel with the most
+    dispatches in this CSV (the timed kernel)."""
+    by = {}
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel in row["Kernel_Name"]:
-                vals.append(float(row["Counter_Value"]))
-    return statistics.median(vals) if vals else None, len(vals)
+            n = short_name(row["Kernel_Name"])
+            if n:
+                by.setdefault(n, []).append(float(row["Counter_Value"]))
+    if not by:
+        return None, None, 0
+    name = max(by, key=lambda k: len(by[k]))
+    return name, statistics.median(by[name]), len(by[name])
 
 
 def main(prof_dir, out_path):
     res = {}
-    for cfg, kern in KERNELS.items():
-        c = cfg[-1]
+    for c in "234":
+        cfg = f"config{c}"
         fpath = os.path.join(prof_dir, f"pmc_FETCH_SIZE_c{c}", "run_counter_collection.csv")
         wpath = os.path.join(prof_dir, f"pmc_WRITE_SIZE_c{c}", "run_counter_collection.csv")
         if not (os.path.exists(fpath) and os.path.exists(wpath)):
             continue
-        fetch, nf = per_launch(fpath, kern)
-        write, nw = per_launch(wpath, kern)
-        if fetch is None or write is None:
+        kern, fetch, nf = per_launch(fpath)
+        kern_w, write, nw = per_launch(wpath)
+        if fetch is None or write is None or kern != kern_w:
             continue
         res[cfg] = {
-            "kernel": NAMES[kern],
+            "kernel": kern,
             "fetch_size_kib": fetch,
             "write_size_kib": write,
             "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),

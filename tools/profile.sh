@@ -11,11 +11,11 @@ cd /tmp
 export TMPDIR=/tmp
 for cfg in 3 2 4; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c$cfg" -o run -- \
-    python3 "$ROOT/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --no-extra \
+    python3 "$ROOT/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --no-extra --no-e2e \
     > "$OUT/bench_c${cfg}_under_trace.json"
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_${ctr}_c$cfg" -o run -- \
-      python3 "$ROOT/bench.py" --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-extra \
+      python3 "$ROOT/bench.py" --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-extra --no-e2e \
       > "$OUT/bench_c${cfg}_pmc_$ctr.json"
   done
 done
