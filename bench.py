@@ -242,15 +242,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
-    if dist:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    # One rank per GPU. YU_BENCH_BACKEND=gloo (rehearsal only) lets several ranks
+    # share fewer GPUs: RCCL refuses two ranks on one device.
+    backend = os.environ.get("YU_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    if dist:
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
 
     w = Workload(args.config, dev, seed=1000 + rank)
     wall, kern = timed(w, args.steps, args.warmup, dist)
-    wall_max = max_over_ranks(wall, device=dev)
+    wall_max = max_over_ranks(wall, device=dev if backend == "nccl" else None)
     ms_per_step = wall_max / args.steps * 1e3
     value = world * w.bytes * args.steps / wall_max / GIB
     achieved = w.bytes / kern / 1e9  # GB/s (decimal, like the peak)
