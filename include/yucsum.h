@@ -128,8 +128,13 @@ uint16_t yu_pseudo_header_checksum(uint32_t protocol,
 
 /* Packets handed to the transport/IPv4/ICMP modes must be <= 65535 bytes
  * (the IPv4 total-length limit; the reference's uint16 length arithmetic is
- * only defined there). RAW mode accepts any length < 2^32. */
+ * only defined there). RAW packets may be up to YU_MAX_RAW_LEN bytes
+ * (4 GiB - 64 KiB; the reference's uint32 wrap is reproduced throughout).
+ * The uniform calls reject longer packets with YU_EINVAL; a ragged batch
+ * is not read back on the host, so a longer ragged packet gets an
+ * unspecified value (never a fault or a hang). */
 #define YU_MAX_TRANSPORT_LEN 65535u
+#define YU_MAX_RAW_LEN 0xFFFF0000u
 
 /* ------------------------------------------------------------------ */
 /* Batched device entry points (the GPU hot path).                     */

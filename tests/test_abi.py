@@ -78,6 +78,7 @@ def test_argument_validation_precedes_device():
     assert L.yu_csum_batch_uniform(p, 16, 16, 4, 0, None, 0, None, None, None) == _lib.YU_EINVAL  # out
     assert L.yu_csum_batch_uniform(p, 16, 70000, 4, 2, None, 0, None, o, None) == _lib.YU_EINVAL  # > 65535
     assert L.yu_csum_batch_uniform(p, 16, 4, 4, 1, None, 0, None, o, None) == _lib.YU_EINVAL  # < UDP header
+    assert L.yu_csum_batch_uniform(p, 16, 0xFFFF0001, 1, 0, None, 0, None, o, None) == _lib.YU_EINVAL  # > YU_MAX_RAW_LEN
     assert L.yu_csum_batch_uniform(p, 16, 16, 0, 0, None, 0, None, o, None) == 0  # empty batch: no-op
     assert L.yu_csum_fill_uniform(p, 16, 16, 4, 0, None, 0, None, o, None) == _lib.YU_EINVAL  # RAW not TX
     assert L.yu_csum_fill_uniform(p + 1, 16, 16, 4, 1, None, 0, None, o, None) == _lib.YU_EINVAL  # unaligned

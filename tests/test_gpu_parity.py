@@ -119,6 +119,62 @@ def test_ragged_all_modes(dev, oracle_c, mode):
         assert np.array_equal(got, want), (mode, use_addrs, np.nonzero(got != want)[0][:10])
 
 
+def _ragged_headers(rng, blob, offs, mode):
+    for p in range(len(offs) - 1):
+        s = int(offs[p])
+        if mode in (O.MODE_TCP, O.MODE_VERIFY_TCP):
+            blob[s + 12] = int(rng.integers(5, 16)) << 4
+        if mode in (O.MODE_IPV4, O.MODE_VERIFY_IPV4):
+            blob[s] = 0x40 | int(rng.integers(0, 16))
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 64), (40, 200), (64, 1500)])
+@pytest.mark.parametrize("mode", list(range(8)))
+def test_ragged_small_packets(dev, oracle_c, mode, lo, hi):
+    """tun-style RX bursts: mostly short packets (k_rag's group path) with a
+    few long ones sprinkled in (its whole-wave phase 2), every start alignment."""
+    rng = np.random.default_rng(7000 + 17 * mode + hi)
+    mn = {O.MODE_UDP: 8, O.MODE_TCP: 60, O.MODE_VERIFY_TCP: 60, O.MODE_ICMP: 4,
+          O.MODE_IPV4: 60, O.MODE_VERIFY_IPV4: 60}.get(mode, 0)
+    n = 5000
+    lens = rng.integers(max(lo, mn), max(hi, mn) + 1, size=n)
+    long_at = rng.choice(n, size=24, replace=False)
+    lens[long_at[:20]] = rng.integers(1537, 9001, size=20)
+    # RAW: past the LE-sum limit; transport/IPv4 modes are capped at 65535
+    lens[long_at[20:]] = rng.integers(131073, 140000, size=4) if mode == O.MODE_RAW else 65535
+    for base_off in (0, 1, 2, 3):
+        blob, offs = _ragged(rng, lens, base_off=base_off)
+        _ragged_headers(rng, blob, offs, mode)
+        addrs = _rand(rng, 8 * n)
+        init = rng.integers(0, 65536, size=n, dtype=np.uint16)
+        got = batch.checksum_ragged(_to(dev, blob), _to(dev, offs.view(np.int64)), mode,
+                                    initial_arr=_to(dev, init), addrs=_to(dev, addrs)).cpu().numpy()
+        want = oracle_c.batch(blob, mode, offsets=offs, initial_arr=init, addrs=addrs)
+        assert np.array_equal(got, want), (base_off, np.nonzero(got != want)[0][:10])
+
+
+@pytest.mark.parametrize("mode", [O.MODE_RAW])
+def test_ragged_far_from_step_base(dev, oracle_c, mode):
+    """A 2.1 GiB packet followed by short ones: the short packets of its step lie
+    more than 1 GiB past the step's first packet, which k_rag's 32-bit lane
+    offsets cannot reach, so they take the whole-wave path; the later steps sit
+    at offsets with bit 31 set (a sign-extension trap for 32-bit lane reads)."""
+    big = (2 << 30) + (100 << 20) + 3
+    lens = np.array([big, 64, 65, 20, 100, 7] + [60] * 10, dtype=np.int64)
+    offs = np.zeros(len(lens) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    offs += 1
+    blob = np.zeros(int(offs[-1]) + 32, np.uint8)
+    rng = np.random.default_rng(77)
+    blob[:1 << 20] = _rand(rng, 1 << 20)
+    blob[-(1 << 20):] = _rand(rng, 1 << 20)
+    _ragged_headers(rng, blob, offs, mode)
+    got = batch.checksum_ragged(_to(dev, blob), _to(dev, offs.view(np.int64)), mode,
+                                initial=0x1234).cpu().numpy()
+    want = oracle_c.batch(blob, mode, offsets=offs, initial=0x1234)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0]
+
+
 def test_ragged_zero_ff_and_empty(dev, oracle_c):
     rng = np.random.default_rng(5)
     lens = np.array([0, 0, 1, 0, 2, 3, 0, 5, 17, 0] + list(rng.integers(0, 300, size=300)))

@@ -2,10 +2,13 @@
 // points on BASELINE configs 2/3/4 with HIP events, without Python/torch in
 // the loop, for quick kernel A/B work and rocprofv3 runs.
 //
-// build: hipcc -O2 -I include tools/kbench.cpp -o tools/kbench -L yustack_amd -lyucsum -Wl,-rpath,'$ORIGIN/../yustack_amd'
+// build: hipcc -O2 --offload-arch=gfx950 -I include tools/kbench.cpp -o tools/kbench -L yustack_amd -lyucsum -Wl,-rpath,'$ORIGIN/../yustack_amd'
 // run:   tools/kbench [config...]   (default 2 3 4)
 #include <hip/hip_runtime.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <stdio.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -28,7 +31,17 @@ __global__ void fill(uint8_t *p, uint64_t n, uint32_t seed) {
   }
 }
 
+static void on_segv(int sig) {
+  void *bt[64];
+  const int k = backtrace(bt, 64);
+  fprintf(stderr, "signal %d\n", sig);
+  backtrace_symbols_fd(bt, k, 2);
+  _exit(128 + sig);
+}
+
 int main(int argc, char **argv) {
+  setvbuf(stdout, nullptr, _IONBF, 0);
+  signal(SIGSEGV, on_segv);
   std::vector<int> cfgs;
   for (int i = 1; i < argc; ++i) cfgs.push_back(atoi(argv[i]));
   if (cfgs.empty()) cfgs = {2, 3, 4};
@@ -51,9 +64,12 @@ int main(int argc, char **argv) {
     uint64_t *d_off = nullptr;
     if (cfg == 2) { L = 64; mode = YU_MODE_RAW; bytes = n * L; alg = bytes + 4 * n; }
     if (cfg == 3) { L = 1500; mode = YU_MODE_TCP; bytes = n * L; alg = bytes + 10 * n; }
-    if (cfg == 4) {
+    if (cfg == 4 || cfg == 5 || cfg == 6) {
+      // 4: BASELINE config 4 (U{64..9000}); 5: tun-like U{64..1500}; 6: U{40..200}
+      const int lo = cfg == 4 ? 64 : (cfg == 5 ? 64 : 40);
+      const int hi = cfg == 4 ? 9000 : (cfg == 5 ? 1500 : 200);
       std::mt19937_64 rng(4);
-      std::uniform_int_distribution<int> d(64, 9000);
+      std::uniform_int_distribution<int> d(lo, hi);
       std::vector<uint64_t> off(n + 1, 0);
       for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + d(rng);
       bytes = off[n];
@@ -85,7 +101,8 @@ int main(int argc, char **argv) {
       double s = ms / 1e3 / reps;
       printf("config%d round %d: %8.1f us/launch  %7.1f GB/s alg  (%.3f of 8 TB/s)  %s\n", cfg, r, s * 1e6,
              alg / s / 1e9, alg / s / 8e12,
-             d_off ? "k_loop<4>" : yu_uniform_variant(L, L, mode, (uintptr_t)bufs[0] & 15));
+             d_off ? (getenv("YU_RAGGED") ? getenv("YU_RAGGED") : "seg")
+                   : yu_uniform_variant(L, L, mode, (uintptr_t)bufs[0] & 15));
     }
     for (auto b : bufs) CK(hipFree(b));
     if (d_off) CK(hipFree(d_off));

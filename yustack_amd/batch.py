@@ -32,6 +32,7 @@ MODES = {"raw": RAW, "udp": UDP, "tcp": TCP, "ipv4": IPV4, "icmp": ICMP,
          "verify_ipv4": VERIFY_IPV4, "verify_tcp": VERIFY_TCP, "verify_udp": VERIFY_UDP}
 TX_MODES = (UDP, TCP, IPV4, ICMP)
 MAX_TRANSPORT_LEN = 65535
+MAX_RAW_LEN = 0xFFFF0000  # include/yucsum.h YU_MAX_RAW_LEN
 
 
 def _mode(m) -> int:
@@ -119,8 +120,10 @@ def checksum_ragged(data: torch.Tensor, offsets: torch.Tensor, mode="raw", *, in
         ok = bool(((o[1:] >= o[:-1]).all() & (o[0] >= 0) & (o[-1] <= data.numel())).item())
         if not ok:
             raise ValueError("offsets are not non-decreasing within data")
-        if m != RAW and bool(((o[1:] - o[:-1]) > MAX_TRANSPORT_LEN).any().item()):
-            raise ValueError("transport/IPv4/ICMP packets must be <= 65535 bytes")
+        cap = MAX_TRANSPORT_LEN if m != RAW else MAX_RAW_LEN
+        if bool(((o[1:] - o[:-1]) > cap).any().item()):
+            raise ValueError("transport/IPv4/ICMP packets must be <= 65535 bytes" if m != RAW
+                             else f"RAW packets must be <= {MAX_RAW_LEN} bytes")
     dev = data.device
     initial_arr = _opt(initial_arr, torch.uint16, n, dev, "initial_arr")
     addrs = _opt(addrs, torch.uint8, 8 * n, dev, "addrs")

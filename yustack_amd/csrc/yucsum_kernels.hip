@@ -274,7 +274,8 @@ __device__ __forceinline__ uint32_t junk_sum(const uint32_t (&x)[3],
 __device__ uint32_t g_side_zero[2] = {0u, 0u};
 
 struct Side {
-  uint32_t a, b, i;
+  uint32_t a, b;
+  uint16_t i;  // 16-bit: widened at its use, not right after its load
 };
 
 struct SidePtrs {
@@ -586,7 +587,8 @@ __device__ __forceinline__ void loop_pkt(const BatchArgs &A, uint64_t p,
   const uint64_t sabs = (uint64_t)(uintptr_t)A.data + k.soff;
   k.base = sabs & ~3ull;
   k.sh = (uint32_t)(sabs & 3u);
-  const uint32_t l32 = (uint32_t)k.len;
+  // ragged packets past the limit get an unspecified value, never a hang
+  const uint32_t l32 = k.len < YU_MAX_RAW_LEN ? (uint32_t)k.len : YU_MAX_RAW_LEN;
   k.E = k.sh + l32;
   k.eload = k.sh + (ipv4 ? (l32 < 60u ? l32 : 60u) : l32);
 }
@@ -686,6 +688,468 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
 }
 
 // ---------------------------------------------------------------------
+// k_rag<G, U, NT>: ragged batches of small packets (tun-style RX bursts,
+// link/tundev/tundev.go:78-151). One packet per wave iteration (k_loop) is
+// latency-bound when packets are a few hundred bytes; here a wave step holds
+// 64/G packets, one per G-lane group, as in k_small, and a 3-stage pipeline
+// keeps the next steps in flight: the offsets of step t+2 and the packet
+// windows of step t+1 are loaded while step t is summed (phase 1). Packets
+// longer than the 16*G*U-byte group window are skipped there and summed in
+// phase 2, after the step loop: each wave scans 64 offsets at a time, ballots
+// the long packets and sums each with all 64 lanes in 4 KiB windows. The two
+// phases do not overlap, so the kernel pays the larger register budget, not
+// the sum.
+// ---------------------------------------------------------------------
+template <int U>
+struct RagItem {
+  uint4 c[U];
+  Side sd;         // side data of the group's packet
+  uint64_t o;      // this lane's offset: offsets[min(pb + lane % (GPW+1), n)]
+  uint32_t len, sh, eload;
+  bool fits;       // this group's packet is summed in phase 1
+};
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Phase 1 takes a packet iff it fits the group window and its window lies
+// within 1 GiB of the step's base (the first packet of its step): lane window
+// offsets are 32-bit. Phase 2 applies the same test and takes the rest.
+__device__ __forceinline__ bool rag_fits(uint32_t need, uint64_t len, uint64_t from_base,
+                                         uint32_t W) {
+  return len <= 0xFFFFFFu && need <= W && from_base < (1ull << 30);
+}
+
+template <int G>
+__device__ __forceinline__ uint64_t rag_offs(const BatchArgs &A, uint64_t pb, uint32_t lane) {
+  constexpr uint32_t GPW = 64u / G;
+  uint64_t i = pb + lane % (GPW + 1u);
+  return A.offsets[i < A.n ? i : A.n];  // unconditional (clamped) load
+}
+
+template <int G, int U, int NT>
+__device__ __forceinline__ void rag_fetch(const BatchArgs &A, const SidePtrs &sp, uint64_t pb,
+                                          uint64_t o, uint32_t gw, uint32_t gl, bool ipv4,
+                                          RagItem<U> &it) {
+  constexpr uint32_t W = 16u * G * U;
+  const uint64_t data = (uint64_t)(uintptr_t)A.data;
+  const uint64_t p = pb + gw;
+  const bool active = p < A.n;
+  const uint64_t so = shfl64(o, gw);
+  const uint64_t eo = shfl64(o, gw + 1u);
+  it.o = o;
+  it.len = active ? (uint32_t)(eo - so) : 0u;
+  const uint64_t sabs = data + so;
+  it.sh = (uint32_t)(sabs & 3u);
+  const uint32_t need = it.sh + (ipv4 ? (it.len < 60u ? it.len : 60u) : it.len);
+  // readfirstlane returns int: widen through uint32_t, never sign-extend
+  const uint64_t o0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(o >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)o);
+  const uint64_t base = uniform64((data + o0) & ~3ull);
+  it.fits = active && rag_fits(need, eo - so, (sabs & ~3ull) - base, W);
+  it.eload = it.fits ? need : 0u;
+  const uint32_t lw = it.fits ? (uint32_t)((sabs & ~3ull) - base) : 0u;
+  const __amdgpu_buffer_rsrc_t r = rsrc_at(base, data + A.offsets[A.n]);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t cr = 16u * (gl + (uint32_t)u * G);
+    it.c[u] = bld16(r, cr < it.eload ? lw + cr : kOOB, nt_step<NT>(u, U));
+  }
+  it.sd = load_side(sp, active ? p : A.n - 1);
+}
+
+// One packet summed by the whole wave in 4 KiB windows, no prefetch: the
+// fallback for steps holding a packet longer than the group window.
+template <bool BE>
+__device__ __forceinline__ uint32_t rag_serial_sum(uint64_t sabs, uint32_t len, uint32_t E,
+                                                   int mode, uint32_t lane, uint64_t end,
+                                                   uint32_t (&jx)[3], const Junk &j) {
+  constexpr uint32_t W = 64u * 16u * 4u;
+  const uint32_t sh = (uint32_t)(sabs & 3u);
+  const uint32_t sel = (sh & 1u) ? kSelIdent : kSelSwap;
+  uint32_t acc = 0;
+  for (uint32_t wb = 0; wb < sh + len; wb += W) {
+    const __amdgpu_buffer_rsrc_t r = rsrc_at(uniform64((sabs & ~3ull) + wb), end);
+    const uint32_t lim = sh + len - wb;
+    uint4 c[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t cr = 16u * (lane + 64u * (uint32_t)u);
+      c[u] = bld16(r, cr < lim ? cr : kOOB, true);
+    }
+    if (wb == 0) junk_take<6>(c[0], 0u, j, jx);
+    if (wb + W <= E) {  // full window (wave-uniform)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = sum_full<BE>(c[u], sel, acc);
+    } else {  // last window: E - wb < W, so the int limits cannot overflow
+      const int f = (int)((E & ~3u) - wb);
+      const int limj[4] = {f, f - 4, f - 8, f - 12};
+      const uint32_t tm = (1u << (8u * (E & 3u))) - 1u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc = sum_masked<BE>(c[u], 16 * (int)(lane + 64u * (uint32_t)u), limj, tm, sel, acc);
+    }
+  }
+  acc = group_total<64>(acc);
+  const uint32_t s = acc - junk_sum<BE>(jx, j, sel);
+  return BE ? s : le_to_be(s, sh & 1u);
+}
+
+template <int G, int U, int NT>
+__global__ __launch_bounds__(256) void k_rag(BatchArgs A) {
+  constexpr uint32_t GPW = 64u / G;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t gl = lane & (G - 1);
+  const uint32_t gw = lane / G;
+  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                        (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t step = (uint64_t)gridDim.x * (blockDim.x >> 6) * GPW;
+  const int mode = A.mode;
+  const bool ipv4 = mode_is_ipv4(mode);
+  const SidePtrs sp = side_ptrs(A);
+  const uint64_t data = (uint64_t)(uintptr_t)A.data;
+  const uint64_t end = data + A.offsets[A.n];
+
+  uint64_t pb = wave * GPW;
+  if (pb >= A.n) return;
+  uint64_t o1 = rag_offs<G>(A, pb + step, lane);
+  RagItem<U> it;
+  rag_fetch<G, U, NT>(A, sp, pb, rag_offs<G>(A, pb, lane), gw, gl, ipv4, it);
+  for (;;) {
+    const uint64_t pn = pb + step;
+    const bool more = pn < A.n;  // wave-uniform
+    const uint64_t o2 = rag_offs<G>(A, pb + 2 * step, lane);
+    RagItem<U> nx;
+    rag_fetch<G, U, NT>(A, sp, more ? pn : A.n, o1, gw, gl, ipv4, nx);
+
+    uint32_t E = it.sh + it.len;
+    if (ipv4) {
+      const uint32_t hl = __shfl(ipv4_hl(it.c[0].x, it.sh), (int)(lane & ~(uint32_t)(G - 1)), 64);
+      E = it.sh + (it.len < hl ? it.len : hl);
+    }
+    const int F = (int)(E & ~3u);
+    const int lim[4] = {F, F - 4, F - 8, F - 12};
+    const uint32_t tm = (1u << (8u * (E & 3u))) - 1u;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cr = 16 * (int)(gl + (uint32_t)u * G);
+      if (__all((int)(!it.fits || cr + 16 <= F)))  // every chunk whole: skip the cut
+        acc = sum_full<false>(it.c[u], 0u, acc);
+      else
+        acc = sum_masked<false>(it.c[u], cr, lim, tm, 0u, acc);
+    }
+    acc = group_total<G>(acc);
+    const Junk j = make_junk(it.sh, E, mode);
+    uint32_t jx[3];
+    junk_take<__builtin_ctz(G)>(it.c[0], lane & ~(uint32_t)(G - 1), j, jx);
+    const uint64_t so = shfl64(it.o, gw);  // all lanes: a cross-lane read needs active sources
+    if (gl == G - 1 && it.fits) {
+      const uint32_t v = le_to_be(acc - junk_sum<false>(jx, j, 0u), it.sh & 1u);
+      finish_packet(A, pb + gw, v, it.len, it.sd, A.fill ? A.fill + so : nullptr, E - it.sh);
+    }
+    if (!more) break;
+    it = nx;
+    o1 = o2;
+    pb = pn;
+  }
+
+  // phase 2: the packets phase 1 skipped (longer than the group window, or
+  // farther than 1 GiB from their step's base), one whole-wave sum each
+  const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  constexpr uint32_t W1 = 16u * G * U;
+  for (uint64_t cb = wave * 64u; cb < A.n; cb += nwave * 64u) {
+    const uint64_t i = cb + lane;
+    const uint64_t ic = i < A.n ? i : A.n - 1;
+    const uint64_t so = A.offsets[ic];
+    const uint64_t eo = A.offsets[ic + 1];
+    const uint64_t bo = A.offsets[ic - ic % GPW];  // its step's base packet
+    const uint64_t sabs = data + so;
+    const uint64_t len = eo - so;
+    const uint32_t l32 = len < 0x0FFFFFFFu ? (uint32_t)len : 0x0FFFFFFFu;
+    const uint32_t need = (uint32_t)(sabs & 3u) + (ipv4 ? (l32 < 60u ? l32 : 60u) : l32);
+    const bool skipped =
+        i < A.n && !rag_fits(need, len, (sabs & ~3ull) - ((data + bo) & ~3ull), W1);
+    uint64_t mask = __ballot((int)skipped);
+    while (mask) {  // wave-uniform
+      const uint32_t q = (uint32_t)__builtin_ctzll(mask);
+      mask &= mask - 1u;
+      const uint64_t ps = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(so >> 32), q) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)so, q);
+      const uint64_t pe = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(eo >> 32), q) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)eo, q);
+      const uint64_t p = cb + q;
+      const uint32_t plen = pe - ps < YU_MAX_RAW_LEN ? (uint32_t)(pe - ps) : YU_MAX_RAW_LEN;
+      const uint64_t pabs = data + ps;
+      const uint32_t sh = (uint32_t)(pabs & 3u);
+      uint32_t E = sh + plen;
+      if (ipv4) {  // only reached for packets far from their step base
+        const __amdgpu_buffer_rsrc_t r = rsrc_at(uniform64(pabs & ~3ull), end);
+        const uint32_t hl = ipv4_hl(__builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 0), sh);
+        E = sh + (plen < hl ? plen : hl);
+      }
+      const Junk j = make_junk(sh, E, mode);
+      uint32_t pjx[3];
+      const uint32_t v = plen > kLEMax ? rag_serial_sum<true>(pabs, E - sh, E, mode, lane, end, pjx, j)
+                                       : rag_serial_sum<false>(pabs, E - sh, E, mode, lane, end, pjx, j);
+      const Side sd = load_side(sp, p);
+      if (lane == 63) finish_packet(A, p, v, plen, sd, A.fill ? A.fill + ps : nullptr, E - sh);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------
+// k_seg<U, NT>: ragged batches as a segmented sum over one byte stream.
+//
+// The packets of a ragged batch tile [offsets[0], offsets[n]) back to back,
+// so a chunk of 64 consecutive packets is one contiguous byte range. A wave
+// takes a chunk (lane l owns packet 64c + l) and streams the range in tiles
+// of 64 lanes x U x 16 bytes — every load a full, coalesced dwordx4 whatever
+// the packet sizes — while keeping P(x), the running LE sum (v_sad_u16) of
+// the chunk's bytes before position x. A packet's sum is P(end) - P(start):
+// prefix differences are exact mod 2^32 and a packet's LE sum stays below
+// 2^32 up to 131072 bytes (the LE-sum limit of the header comment). In TX
+// modes the checksum field is two more points, P(s+f+2) - P(s+f), taken off.
+//
+// Per tile: each lane sums its U chunks, a DPP scan over the wave orders the
+// chunk sums by address, and only if a packet boundary falls in the tile are
+// the chunk bytes and their exclusive prefixes parked in LDS, where each lane
+// whose point lies in the tile reads the one chunk it needs and adds the
+// bytes before the point. Packets larger than a tile cost one scan per tile
+// and no LDS traffic; small packets cost a few LDS reads each instead of a
+// lane group per packet, so HBM sees the same byte stream for any mix.
+//
+// RAW packets longer than 131072 bytes need the reference's exact uint32
+// accumulator (its wrap). A chunk holding one also keeps T(x), the plain byte
+// sum (v_sad_u8): with A/B the sums of the bytes at even/odd addresses,
+// L = A + 256 B and T = A + B (mod 2^32), so B = (L - T) * 255^-1 and A = T - B,
+// and the big-endian word sum is 256 A + B (even start) or A + 256 B (odd
+// start) — bit-exact mod 2^32 at any length.
+//
+// Pipelining: the loads of the next tile — of this chunk, or the first tile
+// of the wave's next chunk, whose offsets and side data were read one chunk
+// ahead — are issued before the current tile is summed.
+// ---------------------------------------------------------------------
+constexpr uint32_t kInv255 = 0xFEFEFEFFu;  // 255 * kInv255 == 1 (mod 2^32)
+
+struct SegChunk {
+  uint64_t p0;      // first packet of the chunk
+  uint64_t ox, oy;  // offsets[] of this lane's packet start / end (clamped to n)
+  uint64_t b0;      // floor4 address of the chunk's first byte (wave-uniform)
+  uint64_t xe;      // chunk end relative to b0 (wave-uniform)
+  Side sd;
+  uint32_t m;       // packets in the chunk (wave-uniform; 0: no chunk)
+};
+
+// Loads only: the offsets and side data of the chunk starting at packet p0.
+__device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
+                                         uint64_t p0, uint32_t lane, SegChunk &k) {
+  const uint64_t n = A.n;
+  const uint64_t i = p0 + lane;
+  k.p0 = p0;
+  k.m = p0 < n ? (uint32_t)(n - p0 < 64u ? n - p0 : 64u) : 0u;
+  k.ox = A.offsets[i < n ? i : n];
+  k.oy = A.offsets[i + 1 < n ? i + 1 : n];
+  k.sd = load_side(sp, i < n ? i : n - 1);
+  k.b0 = (uint64_t)(uintptr_t)A.data & ~3ull;  // set by seg_geom
+  k.xe = 0;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+// Wave-uniform geometry of a loaded chunk (waits for its offsets).
+__device__ __forceinline__ void seg_geom(uint64_t data, SegChunk &k) {
+  if (k.m == 0) return;
+  const uint64_t s = data + readlane64(k.ox, 0);
+  const uint64_t e = data + readlane64(k.oy, 63);  // lane 63's end = offsets[p0 + m]
+  k.b0 = s & ~3ull;
+  k.xe = e - k.b0;
+}
+
+// Loads of tile t (bytes [t*T, t*T + T) past b0) of a chunk ending xe past
+// b0. One call site with selected arguments and a compile-time load policy:
+// no load sits in a branch, so the next tile's loads stay in flight while the
+// current one is summed. (The one 128-byte line two neighbouring chunks share
+// is fetched by both: <= 2% of a chunk of 64 packets >= 40 bytes.)
+template <int U, bool NTL>
+__device__ __forceinline__ void seg_fetch(uint64_t b0, uint64_t xe, uint64_t t, uint32_t lane,
+                                          uint64_t end, uint4 (&c)[U]) {
+  constexpr uint32_t T = 64u * 16u * U;
+  const uint64_t tb = t * T;
+  const __amdgpu_buffer_rsrc_t r = rsrc_at(uniform64(b0 + tb), end);
+  const uint64_t rem = xe > tb ? xe - tb : 0u;
+  const uint32_t lim = rem < T ? (uint32_t)rem : T;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t cr = 16u * (lane + 64u * (uint32_t)u);
+    c[u] = bld16(r, cr < lim ? cr : kOOB, NTL);
+  }
+}
+
+// Sum of the first r (0..15) bytes of a 16-byte chunk: LE halves (sad_u16)
+// or plain bytes (sad_u8).
+template <bool BYTES>
+__device__ __forceinline__ uint32_t seg_part(const uint4 &d, uint32_t r) {
+  const uint32_t w = r >> 2;
+  const uint32_t mk = (1u << (8u * (r & 3u))) - 1u;
+  const uint32_t v[4] = {d.x, d.y, d.z, d.w};
+  uint32_t acc = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t x = j < w ? v[j] : (j == w ? (v[j] & mk) : 0u);
+    acc = BYTES ? __builtin_amdgcn_sad_u8(x, 0u, acc) : sad(x, acc);
+  }
+  return acc;
+}
+
+// One point of a lane: position x (relative to b0), and P / T at x once the
+// tile holding x has gone by.
+struct SegPt {
+  uint64_t x;
+  uint32_t p, t;
+};
+
+template <int U, int NT>
+__global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
+  constexpr uint32_t T = 64u * 16u * U;
+  constexpr uint32_t NC = 64u * U;  // chunks per tile
+  __shared__ uint4 s_data[4][NC];
+  __shared__ uint32_t s_pl[4][NC];
+  __shared__ uint32_t s_pt[4][NC];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const int mode = A.mode;
+  const bool tx = mode_is_tx(mode);
+  const uint32_t fld = mode_field(mode);
+  const SidePtrs sp = side_ptrs(A);
+  const uint64_t data = (uint64_t)(uintptr_t)A.data;
+  const uint64_t end = data + A.offsets[A.n];
+
+  uint64_t ch = wave;
+  if (ch * 64u >= A.n) return;
+  SegChunk cur, nxt;
+  seg_load(A, sp, ch * 64u, lane, cur);
+  seg_load(A, sp, (ch + nwave) * 64u, lane, nxt);
+  seg_geom(data, cur);
+
+  // per-chunk state
+  SegPt pt[4];  // start, end, field start, field end
+  bool exact = false;
+  uint64_t ntiles = 0;
+  uint32_t carry_l = 0, carry_t = 0;
+  auto begin_chunk = [&](const SegChunk &k) {
+    const uint64_t x = data + k.ox - k.b0;
+    const uint64_t y = data + k.oy - k.b0;
+    const uint64_t len = y - x;
+    pt[0].x = x;
+    pt[1].x = y;
+    const bool f = tx && fld + 2u <= len;
+    pt[2].x = f ? x + fld : x;
+    pt[3].x = f ? x + fld + 2u : x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pt[i].p = pt[i].t = 0u;
+    exact = mode == YU_MODE_RAW && __any((int)(len > kLEMax));
+    ntiles = k.xe / T + 1u;
+    carry_l = carry_t = 0u;
+  };
+  begin_chunk(cur);
+
+  uint64_t t = 0;
+  uint4 c[U];
+  seg_fetch<U, NT != 0>(cur.b0, cur.xe, 0, lane, end, c);
+  for (;;) {
+    const bool last = t + 1u == ntiles;  // wave-uniform
+    if (last) seg_geom(data, nxt);
+    uint4 cn[U];
+    seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
+                          end, cn);
+
+    // chunk sums, address-ordered exclusive prefixes (DPP scan per u)
+    const uint64_t tb = t * T;
+    uint32_t pl[U], ptt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t s = sum_full<false>(c[u], 0u, 0u);
+      const uint32_t inc = group_total<64>(s);
+      pl[u] = carry_l + inc - s;
+      carry_l += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    }
+    if (exact) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        uint32_t s = __builtin_amdgcn_sad_u8(c[u].x, 0u, 0u);
+        s = __builtin_amdgcn_sad_u8(c[u].y, 0u, s);
+        s = __builtin_amdgcn_sad_u8(c[u].z, 0u, s);
+        s = __builtin_amdgcn_sad_u8(c[u].w, 0u, s);
+        const uint32_t inc = group_total<64>(s);
+        ptt[u] = carry_t + inc - s;
+        carry_t += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+      }
+    }
+    bool here = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) here |= pt[i].x - tb < T;
+    if (__any((int)here)) {  // a packet boundary lies in this tile
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        s_data[wid][u * 64 + lane] = c[u];
+        s_pl[wid][u * 64 + lane] = pl[u];
+        if (exact) s_pt[wid][u * 64 + lane] = ptt[u];
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint64_t q = pt[i].x - tb;
+        if (q < T) {
+          const uint32_t k = (uint32_t)q >> 4;
+          const uint4 d = s_data[wid][k];
+          pt[i].p = s_pl[wid][k] + seg_part<false>(d, (uint32_t)q & 15u);
+          if (exact) pt[i].t = s_pt[wid][k] + seg_part<true>(d, (uint32_t)q & 15u);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+
+    if (last) {
+      if (lane < cur.m) {
+        const uint32_t odd = (uint32_t)pt[0].x & 1u;
+        uint32_t v;
+        if (exact) {
+          const uint32_t L = pt[1].p - pt[0].p;
+          const uint32_t S = pt[1].t - pt[0].t;
+          const uint32_t b = (L - S) * kInv255;  // odd-address bytes
+          const uint32_t a = S - b;              // even-address bytes
+          v = odd ? a + (b << 8) : (a << 8) + b;
+        } else {
+          v = le_to_be(pt[1].p - pt[0].p - (pt[3].p - pt[2].p), odd);
+        }
+        const uint64_t len = pt[1].x - pt[0].x;
+        finish_packet(A, cur.p0 + lane, v, len, cur.sd, A.fill ? A.fill + cur.ox : nullptr,
+                      (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
+      }
+      if (nxt.m == 0) break;
+      cur = nxt;
+      ch += nwave;
+      seg_load(A, sp, (ch + nwave) * 64u, lane, nxt);
+      begin_chunk(cur);
+      t = 0;
+    } else {
+      ++t;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = cn[u];
+  }
+}
+
+// ---------------------------------------------------------------------
 // Host side: variant selection and launch.
 // ---------------------------------------------------------------------
 typedef void (*KernelFn)(BatchArgs);
@@ -714,6 +1178,18 @@ const Variant kSmall[] = {
 };
 const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, 0, false>, k_loop<4, 1, false>, k_loop<4, 1, false>}, 64, 1};
 const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, 0, true>, k_loop<4, 1, true>, k_loop<4, 1, true>}, 64, 1};
+const Variant kRag = {"k_rag<16,6>", 1536, {k_rag<16, 6, 0>, k_rag<16, 6, 1>, k_rag<16, 6, 2>}, 16, 4};
+const Variant kSeg = {"k_seg<4>", 0, {k_seg<4, 0>, k_seg<4, 1>, k_seg<4, 2>}, 64, 64};
+
+// Ragged kernel choice: the segmented stream sum, except for the IPv4 modes,
+// which read only each packet's header (k_rag's per-packet windows).
+// Measurement override YU_RAGGED=loop|rag|seg.
+const Variant &pick_ragged(int mode) {
+  static const char *f = getenv("YU_RAGGED");
+  if (f && strcmp(f, "loop") == 0) return mode == YU_MODE_RAW ? kLoopBE : kLoopLE;
+  if (mode_is_ipv4(mode) || (f && strcmp(f, "rag") == 0)) return kRag;
+  return kSeg;
+}
 
 // Tuning override (measurement only): YU_VARIANT=<name> forces a k_small
 // variant whenever it covers the shape.
@@ -837,7 +1313,7 @@ int batch_uniform(const uint8_t *data, uint8_t *fill, uint64_t stride,
   if (!data) return YU_EINVAL;
   if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
   if (len < min_len(mode)) return YU_EINVAL;
-  if (len >= 0xFFFFFFF0u) return YU_EINVAL;
+  if (len > YU_MAX_RAW_LEN) return YU_EINVAL;  // window offsets stay in uint32
   // fill: packets must start 4-byte aligned (no dword shared with a
   // neighbour's field)
   if (fill && (((uintptr_t)data | stride) & 3u)) return YU_EINVAL;
@@ -884,9 +1360,9 @@ int batch_ragged(const uint8_t *data, uint8_t *fill, const uint64_t *offsets,
   A.initial = initial;
   A.uf = 0;
   A.mode = mode;
-  // RAW packets may exceed 131072 bytes: the exact BE sum; transport/IPv4/
-  // ICMP packets are <= 65535 bytes by contract: the LE sum.
-  return launch(mode == YU_MODE_RAW ? kLoopBE : kLoopLE, A, (hipStream_t)stream);
+  // k_seg streams the batch's bytes (exact BE recovery for chunks holding a
+  // RAW packet > 131072 bytes); k_rag takes the IPv4 header-only modes.
+  return launch(pick_ragged(mode), A, (hipStream_t)stream);
 }
 
 }  // namespace
