@@ -81,6 +81,15 @@ const (
 	ModeVerifyIPv4 Mode = C.YU_MODE_VERIFY_IPV4
 	ModeVerifyTCP  Mode = C.YU_MODE_VERIFY_TCP
 	ModeVerifyUDP  Mode = C.YU_MODE_VERIFY_UDP
+	ModeVerifyRX   Mode = C.YU_MODE_VERIFY_RX // out[i] = RX* bits
+)
+
+// VERIFY_RX result bits (include/yucsum.h YU_RX_*).
+const (
+	RXIPOk    = C.YU_RX_IP_OK
+	RXL4      = C.YU_RX_L4
+	RXL4Ok    = C.YU_RX_L4_OK
+	RXInvalid = C.YU_RX_INVALID
 )
 
 // ErrNoDevice is returned when no MI355X (HIP device) is usable.

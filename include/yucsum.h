@@ -124,7 +124,26 @@ uint16_t yu_pseudo_header_checksum(uint32_t protocol,
  * never verifies on receive (transport/udp/endpoint.go:191-229); this is
  * the checker.TCP formula applied to UDP. */
 #define YU_MODE_VERIFY_UDP 7
-#define YU_MODE_COUNT 8
+/* Receive-side verification of whole IPv4 packets as a tun device delivers
+ * them (link/tundev/tundev.go:78-114 -> network/ipv4/ipv4.go:62-77): the
+ * composition of checker.IPv4 and checker.TCP's checksum test
+ * (checker/checker.go:25-40,71-92), all inputs taken from the packet itself:
+ *   valid  = len >= 20 && HeaderLength() <= TotalLength() <= len
+ *            (IPv4.IsValid, header/ipv4.go:126-138)
+ *   IP ok  = Checksum(b[:HeaderLength()], 0) in {0, 0xFFFF}
+ *   L4     = valid && Protocol() in {6 TCP, 17 UDP, 1 ICMP}
+ *   L4 ok  = Checksum(Payload(), Checksum(BE16(len(Payload())),
+ *            PseudoHeaderChecksum(proto, src, dst))) in {0, 0xFFFF}, with
+ *            Payload() = b[HeaderLength():TotalLength()]; ICMP without the
+ *            pseudo-header and length (network/ipv4/icmp.go:36-45).
+ * out[i] is a bit set of YU_RX_*. No side arrays; not a fill mode. */
+#define YU_MODE_VERIFY_RX 8
+#define YU_MODE_COUNT 9
+
+#define YU_RX_IP_OK 1u   /* header checksum verifies */
+#define YU_RX_L4 2u      /* transport (TCP/UDP/ICMP) present and checked */
+#define YU_RX_L4_OK 4u   /* transport checksum verifies */
+#define YU_RX_INVALID 8u /* IPv4.IsValid fails (nothing else is set) */
 
 /* Packets handed to the transport/IPv4/ICMP modes must be <= 65535 bytes
  * (the IPv4 total-length limit; the reference's uint16 length arithmetic is

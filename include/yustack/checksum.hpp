@@ -212,6 +212,7 @@ enum Mode : int {
   VERIFY_IPV4 = YU_MODE_VERIFY_IPV4,
   VERIFY_TCP = YU_MODE_VERIFY_TCP,
   VERIFY_UDP = YU_MODE_VERIFY_UDP,
+  VERIFY_RX = YU_MODE_VERIFY_RX,  // out[i] = YU_RX_* bits
 };
 
 struct Side {

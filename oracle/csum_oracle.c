@@ -35,6 +35,11 @@
 #define OR_MODE_VERIFY_IPV4 5
 #define OR_MODE_VERIFY_TCP 6
 #define OR_MODE_VERIFY_UDP 7
+#define OR_MODE_VERIFY_RX 8
+#define OR_RX_IP_OK 1
+#define OR_RX_L4 2
+#define OR_RX_L4_OK 4
+#define OR_RX_INVALID 8
 
 /* checksum/checksum.go:32-35 — ChecksumCombine */
 uint16_t or_checksum_combine(uint16_t a, uint16_t b) {
@@ -148,7 +153,9 @@ uint16_t or_packet(int mode, const uint8_t *pkt, uint64_t len,
       size_t cp = len < sizeof(hdr) ? (size_t)len : sizeof(hdr);
       memcpy(hdr, pkt, cp);
       if (cp >= 12) hdr[10] = hdr[11] = 0; /* Encode: Checksum zero value */
-      return (uint16_t)~or_ipv4_calculate_checksum(hdr);
+      /* b[:IHL*4], clamped to the packet as a Go slice of it would be */
+      size_t hl = cp ? (size_t)(hdr[0] & 0xf) * 4 : 0;
+      return (uint16_t)~or_checksum(hdr, hl < cp ? hl : cp, 0);
     }
     case OR_MODE_ICMP: {
       /* network/ipv4/icmp.go:36-45 */
@@ -157,9 +164,11 @@ uint16_t or_packet(int mode, const uint8_t *pkt, uint64_t len,
       uint16_t inner = or_checksum(pkt + 4, (size_t)(len - 4), 0);
       return (uint16_t)~or_checksum(hdr, 4, inner);
     }
-    case OR_MODE_VERIFY_IPV4:
-      /* checker/checker.go:32 */
-      return or_ipv4_calculate_checksum(pkt);
+    case OR_MODE_VERIFY_IPV4: {
+      /* checker/checker.go:32; b[:IHL*4] clamped to the packet */
+      size_t hl = len ? (size_t)(pkt[0] & 0xf) * 4 : 0;
+      return or_checksum(pkt, hl < len ? hl : (size_t)len, 0);
+    }
     case OR_MODE_VERIFY_TCP:
     case OR_MODE_VERIFY_UDP: {
       /* checker/checker.go:80-88 */
@@ -169,6 +178,36 @@ uint16_t or_packet(int mode, const uint8_t *pkt, uint64_t len,
       uint8_t lb[2] = {(uint8_t)(l >> 8), (uint8_t)l};
       xsum = or_checksum(lb, 2, xsum);
       return or_checksum(pkt, (size_t)len, xsum);
+    }
+    case OR_MODE_VERIFY_RX: {
+      /* A received IPv4 packet checked as checker.IPv4 + checker.TCP do
+       * (checker/checker.go:25-40,71-92), addresses, protocol and lengths
+       * read from the packet itself (header/ipv4.go:91-138,182-189). */
+      if (len < 20) return OR_RX_INVALID;               /* IsValid: minimum */
+      size_t hl = (size_t)(pkt[0] & 0xf) * 4;           /* HeaderLength() */
+      size_t tl = ((size_t)pkt[2] << 8) | pkt[3];       /* TotalLength() */
+      if (hl > tl || tl > len) return OR_RX_INVALID;    /* IsValid */
+      uint16_t r = 0;
+      uint16_t x = or_checksum(pkt, hl, 0);             /* CalculateChecksum */
+      if (x == 0 || x == 0xffff) r |= OR_RX_IP_OK;
+      uint8_t proto = pkt[9];                           /* Protocol() */
+      if (proto == 6 || proto == 17 || proto == 1) {
+        r |= OR_RX_L4;
+        const uint8_t *pl = pkt + hl;                   /* Payload() */
+        size_t plen = tl - hl;
+        uint16_t xs;
+        if (proto == 1) {
+          xs = or_checksum(pl, plen, 0);                /* ICMP: no pseudo */
+        } else {
+          uint16_t l = (uint16_t)plen;
+          xs = or_pseudo_header_checksum(proto, pkt + 12, 4, pkt + 16, 4);
+          uint8_t lb[2] = {(uint8_t)(l >> 8), (uint8_t)l};
+          xs = or_checksum(lb, 2, xs);
+          xs = or_checksum(pl, plen, xs);
+        }
+        if (xs == 0 || xs == 0xffff) r |= OR_RX_L4_OK;
+      }
+      return r;
     }
     default:
       return 0;

@@ -30,12 +30,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libcsum_oracle.so")
 
 MODE_RAW, MODE_UDP, MODE_TCP, MODE_IPV4, MODE_ICMP = 0, 1, 2, 3, 4
-MODE_VERIFY_IPV4, MODE_VERIFY_TCP, MODE_VERIFY_UDP = 5, 6, 7
+MODE_VERIFY_IPV4, MODE_VERIFY_TCP, MODE_VERIFY_UDP, MODE_VERIFY_RX = 5, 6, 7, 8
 MODE_NAMES = {
     MODE_RAW: "raw", MODE_UDP: "udp", MODE_TCP: "tcp", MODE_IPV4: "ipv4",
     MODE_ICMP: "icmp", MODE_VERIFY_IPV4: "verify_ipv4",
     MODE_VERIFY_TCP: "verify_tcp", MODE_VERIFY_UDP: "verify_udp",
+    MODE_VERIFY_RX: "verify_rx",
 }
+RX_IP_OK, RX_L4, RX_L4_OK, RX_INVALID = 1, 2, 4, 8  # include/yucsum.h YU_RX_*
 
 
 # --------------------------------------------------------------------------
@@ -155,6 +157,29 @@ def packet(mode: int, pkt: bytes, initial_arr=None, initial: int = 0, addrs=None
         xsum = _pseudo(proto, addrs, initial_arr, initial, p)
         xsum = checksum(bytes([l >> 8, l & 0xFF]), xsum)
         return checksum(pkt, xsum)
+    if mode == MODE_VERIFY_RX:  # checker/checker.go:25-40,71-92 on a received packet
+        if len(pkt) < 20:
+            return RX_INVALID
+        hl = (pkt[0] & 0xF) * 4
+        tl = (pkt[2] << 8) | pkt[3]
+        if hl > tl or tl > len(pkt):
+            return RX_INVALID
+        r = 0
+        if ipv4_calculate_checksum(pkt) in (0, 0xFFFF):
+            r |= RX_IP_OK
+        proto = pkt[9]
+        if proto in (1, 6, 17):
+            r |= RX_L4
+            payload = pkt[hl:tl]
+            if proto == 1:
+                xs = checksum(payload, 0)
+            else:
+                xs = pseudo_header_checksum(proto, pkt[12:16], pkt[16:20])
+                xs = checksum(bytes([(len(payload) >> 8) & 0xFF, len(payload) & 0xFF]), xs)
+                xs = checksum(payload, xs)
+            if xs in (0, 0xFFFF):
+                r |= RX_L4_OK
+        return r
     raise ValueError(f"bad mode {mode}")
 
 

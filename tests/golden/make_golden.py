@@ -30,6 +30,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
+
 from oracle import oracle as O  # noqa: E402
 
 EDGE_LENS = [0, 1, 2, 3, 15, 16, 17, 63, 64, 65, 1499, 1500, 1501, 8999, 9000]
@@ -171,7 +173,6 @@ def main() -> None:
     addrs = pattern("rand", 8 * len(lens), rng)
     init = [rng.getrandbits(16) for _ in lens]
     modes = {}
-    import numpy as np
     for m, name in O.MODE_NAMES.items():
         want_a = O.batch_ragged_py(bytes(blob), offs, m, addrs=addrs if m in (1, 2, 6, 7) else None)
         want_i = O.batch_ragged_py(bytes(blob), offs, m, initial_arr=init)
@@ -182,16 +183,39 @@ def main() -> None:
         assert (want_a == c_a).all() and (want_i == c_i).all(), name
         modes[name] = {"with_addrs": [int(x) for x in want_a], "with_initial": [int(x) for x in want_i]}
 
+    # VERIFY_RX (whole received datagrams): the harness packets above are what the
+    # reference's tests feed checker.IPv4/checker.TCP, so each must come out
+    # IP_OK | L4 | L4_OK; damaged copies and the published header pin the rest.
+    rx = []
+    for h in harness:
+        pk = bytes.fromhex(h["hex"])
+        variants = [("as built", pk)]
+        b = bytearray(pk); b[25] ^= 0x01; variants.append(("transport byte flipped", bytes(b)))
+        b = bytearray(pk); b[8] ^= 0x80; variants.append(("ttl flipped", bytes(b)))
+        variants.append(("trailing bytes", pk + b"\x00\x01\x02"))
+        variants.append(("truncated", pk[:-1]))
+        for what, d in variants:
+            want = O.packet(O.MODE_VERIFY_RX, d)
+            assert want == C.batch(np.frombuffer(d, np.uint8), O.MODE_VERIFY_RX,
+                                   offsets=np.array([0, len(d)], np.uint64))[0]
+            rx.append({"what": f"{h['proto']} harness, {what}", "hex": d.hex(), "want": want})
+    assert all(r["want"] == 7 for r in rx if r["what"].endswith("as built"))
+    hdr = bytes.fromhex("4500007300004000" "4011b861c0a80001c0a800c7")
+    rx.append({"what": "published header + 95 zero bytes", "hex": (hdr + bytes(95)).hex(),
+               "want": O.packet(O.MODE_VERIFY_RX, hdr + bytes(95))})
+    assert rx[-1]["want"] & O.RX_IP_OK
+
     out = {
         "generator": "tests/golden/make_golden.py (oracle/oracle.py twin, cross-checked vs oracle/csum_oracle.c)",
         "published": published, "raw": raw, "wrap": wrap, "pseudo": pseudo, "harness": harness,
         "batch": {"hex": bytes(blob).hex(), "offsets": offs, "addrs": addrs.hex(), "initial": init,
                   "modes": modes},
+        "rx": rx,
     }
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(f"wrote {len(raw)} raw, {len(wrap)} wrap, {len(pseudo)} pseudo, {len(harness)} harness, "
-          f"{len(modes)} batch-mode vectors")
+          f"{len(modes)} batch-mode, {len(rx)} rx vectors")
 
 
 if __name__ == "__main__":

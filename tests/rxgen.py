@@ -1,0 +1,90 @@
+"""Received-packet batches for the VERIFY_RX mode (test data, not product).
+
+Packets are whole IPv4 datagrams as a tun device delivers them
+(link/tundev/tundev.go:78-114): an IPv4 header (IHL 5..15, options random) and a
+TCP, UDP, ICMP or other payload, with both checksums filled the way the
+reference's senders fill them (network/ipv4/ipv4.go:80-97 for the header;
+transport/tcp/connect.go:556-586, transport/udp/endpoint.go:164-187,
+network/ipv4/icmp.go:36-45 for the transport). A share of them is then damaged
+— a flipped header or payload byte, a wrong total length, a truncated packet,
+trailing bytes past the total length — so every YU_RX_* outcome occurs.
+The expected flags always come from the oracle, never from this generator.
+"""
+import numpy as np
+
+from oracle import oracle as O
+
+
+def _fill16(buf, off, value):
+    buf[off] = (value >> 8) & 0xFF
+    buf[off + 1] = value & 0xFF
+
+
+def make_packet(rng, plen, proto=None, ihl=None):
+    proto = int(rng.choice([6, 17, 1, 47])) if proto is None else proto
+    ihl = int(rng.integers(5, 16)) if ihl is None else ihl
+    hl = 4 * ihl
+    if proto == 6:
+        plen = max(plen, 20)
+    elif proto == 17:
+        plen = max(plen, 8)
+    elif proto == 1:
+        plen = max(plen, 4)
+    tl = hl + plen
+    pkt = bytearray(rng.integers(0, 256, size=tl, dtype=np.uint8).tobytes())
+    pkt[0] = 0x40 | ihl
+    _fill16(pkt, 2, tl)
+    pkt[9] = proto
+    pkt[10] = pkt[11] = 0
+    _fill16(pkt, 10, ~O.checksum(bytes(pkt[:hl]), 0) & 0xFFFF)
+    src, dst = bytes(pkt[12:16]), bytes(pkt[16:20])
+    seg = hl
+    if proto == 6:
+        pkt[seg + 12] = int(rng.integers(5, min(15, plen // 4) + 1)) << 4
+        pkt[seg + 16] = pkt[seg + 17] = 0
+        xs = O.pseudo_header_checksum(6, src, dst)
+        xs = O.checksum(bytes([(plen >> 8) & 0xFF, plen & 0xFF]), xs)
+        _fill16(pkt, seg + 16, ~O.checksum(bytes(pkt[seg:]), xs) & 0xFFFF)
+    elif proto == 17:
+        _fill16(pkt, seg + 4, plen)
+        pkt[seg + 6] = pkt[seg + 7] = 0
+        xs = O.pseudo_header_checksum(17, src, dst)
+        xs = O.checksum(bytes([(plen >> 8) & 0xFF, plen & 0xFF]), xs)
+        _fill16(pkt, seg + 6, ~O.checksum(bytes(pkt[seg:]), xs) & 0xFFFF)
+    elif proto == 1:
+        pkt[seg + 2] = pkt[seg + 3] = 0
+        _fill16(pkt, seg + 2, ~O.checksum(bytes(pkt[seg:]), 0) & 0xFFFF)
+    return pkt
+
+
+def damage(rng, pkt):
+    r = rng.random()
+    hl = (pkt[0] & 0xF) * 4
+    if r < 0.15:  # header byte
+        i = int(rng.integers(0, hl))
+        pkt[i] ^= 1 << int(rng.integers(0, 8))
+    elif r < 0.30 and len(pkt) > hl:  # payload byte
+        i = int(rng.integers(hl, len(pkt)))
+        pkt[i] ^= 1 << int(rng.integers(0, 8))
+    elif r < 0.35:  # total length beyond the packet
+        _fill16(pkt, 2, len(pkt) + int(rng.integers(1, 100)))
+    elif r < 0.38:  # truncated below the minimum header
+        del pkt[int(rng.integers(0, 20)):]
+    elif r < 0.41:  # total length below the header length
+        _fill16(pkt, 2, int(rng.integers(0, hl)))
+    elif r < 0.50:  # trailing bytes past the total length (IsValid accepts)
+        pkt += bytes(rng.integers(0, 256, size=int(rng.integers(1, 64)), dtype=np.uint8))
+    return pkt
+
+
+def rx_batch(rng, n, lo=0, hi=1480, bad=0.5):
+    """Ragged blob + offsets of n received packets with payloads in [lo, hi]."""
+    pkts = []
+    for _ in range(n):
+        p = make_packet(rng, int(rng.integers(lo, hi + 1)))
+        if rng.random() < bad:
+            p = damage(rng, p)
+        pkts.append(bytes(p))
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in pkts])
+    return np.frombuffer(b"".join(pkts), dtype=np.uint8).copy(), offs

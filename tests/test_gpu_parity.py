@@ -175,6 +175,41 @@ def test_ragged_far_from_step_base(dev, oracle_c, mode):
     assert np.array_equal(got, want), np.nonzero(got != want)[0]
 
 
+@pytest.mark.parametrize("lo,hi", [(0, 40), (0, 300), (0, 1480), (1000, 9000)])
+def test_verify_rx_ragged(dev, oracle_c, lo, hi):
+    """Whole received datagrams (tun RX bursts): header + transport verification
+    bits against the oracle, every start alignment, valid and damaged packets."""
+    import rxgen
+    rng = np.random.default_rng(9100 + hi)
+    blob, offs = rxgen.rx_batch(rng, 3000, lo=lo, hi=min(hi, 65535 - 80))
+    for base_off in (0, 1, 2, 3):
+        b = np.concatenate([np.zeros(base_off, np.uint8), blob, np.zeros(32, np.uint8)])
+        o = offs + base_off
+        got = batch.checksum_ragged(_to(dev, b), _to(dev, o.view(np.int64)), "verify_rx").cpu().numpy()
+        want = oracle_c.batch(b, O.MODE_VERIFY_RX, offsets=o)
+        assert np.array_equal(got, want), (base_off, np.nonzero(got != want)[0][:10])
+    assert len(np.unique(want)) >= 5
+
+
+@pytest.mark.parametrize("length", [20, 40, 64, 576, 1500])
+def test_verify_rx_uniform(dev, oracle_c, length):
+    """Fixed-size received datagrams in uniform slots (stride >= length)."""
+    import rxgen
+    rng = np.random.default_rng(9200 + length)
+    n, stride = 777, length + 5
+    host = np.zeros(n * stride + 64, np.uint8)
+    for p in range(n):
+        pk = rxgen.make_packet(rng, length - 20, ihl=5)
+        if rng.random() < 0.4:
+            pk = rxgen.damage(rng, pk)
+        pk = bytes(pk[:length]).ljust(length, b"\0")
+        host[p * stride: p * stride + length] = np.frombuffer(pk, np.uint8)
+    for base_off in (0, 2):
+        got = batch.checksum_uniform(_to(dev, host[base_off:]), stride, length, n - 1, "verify_rx").cpu().numpy()
+        want = oracle_c.batch(host[base_off:], O.MODE_VERIFY_RX, stride=stride, length=length, n=n - 1)
+        assert np.array_equal(got, want), (base_off, np.nonzero(got != want)[0][:10])
+
+
 def test_ragged_zero_ff_and_empty(dev, oracle_c):
     rng = np.random.default_rng(5)
     lens = np.array([0, 0, 1, 0, 2, 3, 0, 5, 17, 0] + list(rng.integers(0, 300, size=300)))

@@ -18,6 +18,9 @@ ICMP           field value of sendICMPv4                       network/ipv4/icmp
 VERIFY_IPV4    checker.IPv4 sum (valid iff 0 or 0xFFFF)        checker/checker.go:25-40
 VERIFY_TCP     checker.TCP sum                                 checker/checker.go:71-99
 VERIFY_UDP     the checker.TCP formula for UDP
+VERIFY_RX      whole received IPv4 packets: IsValid + checker.IPv4 + checker.TCP's
+               test, inputs read from each packet; out = YU_RX_* bits
+                                                               checker/checker.go:25-99
 =============  =========================================================================
 """
 from __future__ import annotations
@@ -27,9 +30,12 @@ import torch
 
 from ._lib import check, lib
 
-RAW, UDP, TCP, IPV4, ICMP, VERIFY_IPV4, VERIFY_TCP, VERIFY_UDP = range(8)
+RAW, UDP, TCP, IPV4, ICMP, VERIFY_IPV4, VERIFY_TCP, VERIFY_UDP, VERIFY_RX = range(9)
 MODES = {"raw": RAW, "udp": UDP, "tcp": TCP, "ipv4": IPV4, "icmp": ICMP,
-         "verify_ipv4": VERIFY_IPV4, "verify_tcp": VERIFY_TCP, "verify_udp": VERIFY_UDP}
+         "verify_ipv4": VERIFY_IPV4, "verify_tcp": VERIFY_TCP, "verify_udp": VERIFY_UDP,
+         "verify_rx": VERIFY_RX}
+# VERIFY_RX result bits (include/yucsum.h YU_RX_*)
+RX_IP_OK, RX_L4, RX_L4_OK, RX_INVALID = 1, 2, 4, 8
 TX_MODES = (UDP, TCP, IPV4, ICMP)
 MAX_TRANSPORT_LEN = 65535
 MAX_RAW_LEN = 0xFFFF0000  # include/yucsum.h YU_MAX_RAW_LEN
@@ -37,7 +43,7 @@ MAX_RAW_LEN = 0xFFFF0000  # include/yucsum.h YU_MAX_RAW_LEN
 
 def _mode(m) -> int:
     m = MODES[m] if isinstance(m, str) else int(m)
-    if not 0 <= m < 8:
+    if not 0 <= m < len(MODES):
         raise ValueError(f"bad mode {m}")
     return m
 
@@ -177,6 +183,15 @@ def verified(sums: torch.Tensor) -> torch.Tensor:
     """checker semantics: a VERIFY_* sum is valid iff it is 0x0000 or 0xFFFF."""
     s = sums.view(torch.int16)
     return (s == 0) | (s == -1)
+
+
+def rx_accepted(flags: torch.Tensor) -> torch.Tensor:
+    """VERIFY_RX: the packet is well formed, its header checksum verifies and, when
+    it carries TCP/UDP/ICMP, so does the transport checksum."""
+    f = flags.to(torch.int32)
+    ok_ip = (f & (RX_IP_OK | RX_INVALID)) == RX_IP_OK
+    ok_l4 = ((f & RX_L4) == 0) | ((f & RX_L4_OK) != 0)
+    return ok_ip & ok_l4
 
 
 def variant(stride: int, length: int, mode="raw", align16: int = 0) -> str:

@@ -937,22 +937,30 @@ constexpr uint32_t kInv255 = 0xFEFEFEFFu;  // 255 * kInv255 == 1 (mod 2^32)
 
 struct SegChunk {
   uint64_t p0;      // first packet of the chunk
-  uint64_t ox, oy;  // offsets[] of this lane's packet start / end (clamped to n)
+  uint64_t ox, oy;  // this lane's packet [ox, oy) as offsets into data (lanes
+                    // past the batch: the chunk end)
   uint64_t b0;      // floor4 address of the chunk's first byte (wave-uniform)
   uint64_t xe;      // chunk end relative to b0 (wave-uniform)
   Side sd;
-  uint32_t m;       // packets in the chunk (wave-uniform; 0: no chunk)
 };
 
-// Loads only: the offsets and side data of the chunk starting at packet p0.
+// Loads only: the packet bounds and side data of the chunk starting at
+// packet p0. Ragged: offsets[]; uniform: i*stride (packets may leave gaps,
+// which are streamed but belong to no packet, or overlap).
 __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
                                          uint64_t p0, uint32_t lane, SegChunk &k) {
   const uint64_t n = A.n;
   const uint64_t i = p0 + lane;
   k.p0 = p0;
-  k.m = p0 < n ? (uint32_t)(n - p0 < 64u ? n - p0 : 64u) : 0u;
-  k.ox = A.offsets[i < n ? i : n];
-  k.oy = A.offsets[i + 1 < n ? i + 1 : n];
+  // ragged: two (clamped) offset loads; uniform: arithmetic, with lanes past
+  // the batch at the chunk's end (its last packet's end)
+  const uint64_t last = p0 < n ? (n - p0 < 64u ? n : p0 + 64u) - 1u : 0u;
+  const uint64_t uy = (i < n ? i : last) * A.stride + A.len;
+  const uint64_t *offs = A.offsets ? A.offsets : (const uint64_t *)g_side_zero;
+  const uint64_t ry = offs[A.offsets ? (i + 1 < n ? i + 1 : n) : 0];
+  const uint64_t rx = offs[A.offsets ? (i < n ? i : n) : 0];
+  k.ox = A.offsets ? rx : (i < n ? i * A.stride : uy);
+  k.oy = A.offsets ? ry : uy;
   k.sd = load_side(sp, i < n ? i : n - 1);
   k.b0 = (uint64_t)(uintptr_t)A.data & ~3ull;  // set by seg_geom
   k.xe = 0;
@@ -964,10 +972,10 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
 }
 
 // Wave-uniform geometry of a loaded chunk (waits for its offsets).
-__device__ __forceinline__ void seg_geom(uint64_t data, SegChunk &k) {
-  if (k.m == 0) return;
+__device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, SegChunk &k) {
+  if (k.p0 >= n) return;  // no such chunk
   const uint64_t s = data + readlane64(k.ox, 0);
-  const uint64_t e = data + readlane64(k.oy, 63);  // lane 63's end = offsets[p0 + m]
+  const uint64_t e = data + readlane64(k.oy, 63);  // lane 63's end = the chunk end
   k.b0 = s & ~3ull;
   k.xe = e - k.b0;
 }
@@ -1015,13 +1023,50 @@ struct SegPt {
   uint32_t p, t;
 };
 
-template <int U, int NT>
+// RX verification (YU_MODE_VERIFY_RX): the IPv4 header of a received packet
+// fixes two more points — the header end and the transport end — and the
+// pseudo-header. Its first 20 bytes (up to 6 dwords from floor4(start)) are
+// gathered from the tiles' LDS copies as they go by (a header may straddle
+// two tiles), then parsed.
+struct SegRx {
+  uint32_t h[6];    // header window dwords
+  uint32_t need;    // mask of the window dwords still to gather (0: parsed)
+  uint32_t flags;   // YU_RX_* bits known at parse time
+  uint32_t pseudo;  // LE-free big-endian word sum of src, dst, proto, length
+  uint32_t proto;
+};
+
+// Parse the gathered header of a packet of length len starting sh = start&3
+// bytes into h[0] (header/ipv4.go:91-118,126-138). Returns the header and
+// total lengths through hl/tl.
+__device__ __forceinline__ void rx_parse(SegRx &rx, uint32_t sh, uint64_t len, uint32_t &hl,
+                                         uint32_t &tl) {
+  uint32_t w[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j)  // bytes 4j..4j+3 of the header
+    w[j] = sh ? __builtin_amdgcn_alignbyte(rx.h[j + 1], rx.h[j], sh) : rx.h[j];
+  hl = (w[0] & 0xFu) * 4u;                                // HeaderLength()
+  tl = ((w[0] >> 8) & 0xFF00u) | (w[0] >> 24);            // TotalLength(), BE
+  const uint32_t proto = (w[2] >> 8) & 0xFFu;             // Protocol()
+  const bool valid = hl <= tl && tl <= len;               // IsValid (len >= 20 checked)
+  const bool l4 = valid && (proto == 6u || proto == 17u || proto == 1u);
+  rx.flags = valid ? 0u : YU_RX_INVALID;
+  if (l4) rx.flags |= YU_RX_L4;
+  rx.proto = proto;
+  // PseudoHeaderChecksum(proto, src, dst) + BE16(len(payload))
+  // (checker/checker.go:80-88); ICMP has none (network/ipv4/icmp.go:36-45)
+  uint32_t ph = sadperm(w[3], kSelSwap, 0u);
+  ph = sadperm(w[4], kSelSwap, ph);
+  rx.pseudo = proto == 1u ? 0u : ph + proto + ((tl - hl) & 0xFFFFu);
+  if (!valid) hl = tl = 0;
+}
+
+template <int U, int NT, bool RX>
 __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   constexpr uint32_t T = 64u * 16u * U;
   constexpr uint32_t NC = 64u * U;  // chunks per tile
-  __shared__ uint4 s_data[4][NC];
-  __shared__ uint32_t s_pl[4][NC];
-  __shared__ uint32_t s_pt[4][NC];
+  __shared__ uint4 s_data[4][NC];   // the tile's bytes
+  __shared__ uint32_t s_pre[4][NC];  // chunk-exclusive prefixes (L, then T)
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
@@ -1031,21 +1076,22 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   const uint32_t fld = mode_field(mode);
   const SidePtrs sp = side_ptrs(A);
   const uint64_t data = (uint64_t)(uintptr_t)A.data;
-  const uint64_t end = data + A.offsets[A.n];
+  const uint64_t end = A.offsets ? data + A.offsets[A.n] : A.end;
+  const uint32_t *s_dw = (const uint32_t *)s_data[wid];
 
   uint64_t ch = wave;
   if (ch * 64u >= A.n) return;
   SegChunk cur, nxt;
   seg_load(A, sp, ch * 64u, lane, cur);
   seg_load(A, sp, (ch + nwave) * 64u, lane, nxt);
-  seg_geom(data, cur);
+  seg_geom(data, A.n, cur);
 
   // per-chunk state
-  SegPt pt[4];  // start, end, field start, field end
+  SegPt pt[4];  // start, end, then field start/end (TX) or header/transport end (RX)
+  SegRx rx;
   bool exact = false;
-  uint64_t ntiles = 0;
   uint32_t carry_l = 0, carry_t = 0;
-  auto begin_chunk = [&](const SegChunk &k) {
+  auto begin_chunk = [&](const SegChunk &k) __attribute__((always_inline)) {
     const uint64_t x = data + k.ox - k.b0;
     const uint64_t y = data + k.oy - k.b0;
     const uint64_t len = y - x;
@@ -1054,21 +1100,35 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
     const bool f = tx && fld + 2u <= len;
     pt[2].x = f ? x + fld : x;
     pt[3].x = f ? x + fld + 2u : x;
+    if (RX) {  // derived points unknown until the header is parsed
+      pt[2].x = pt[3].x = ~0ull;
+      const uint32_t sh = (uint32_t)x & 3u;
+      rx.need = len >= 20u ? (1u << (((19u + sh) >> 2) + 1u)) - 1u : 0u;
+      rx.flags = YU_RX_INVALID;
+      rx.pseudo = rx.proto = 0u;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
+      if (!rx.need) pt[2].x = pt[3].x = x;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) pt[i].p = pt[i].t = 0u;
     exact = mode == YU_MODE_RAW && __any((int)(len > kLEMax));
-    ntiles = k.xe / T + 1u;
     carry_l = carry_t = 0u;
   };
   begin_chunk(cur);
 
   uint64_t t = 0;
-  uint4 c[U];
-  seg_fetch<U, NT != 0>(cur.b0, cur.xe, 0, lane, end, c);
-  for (;;) {
-    const bool last = t + 1u == ntiles;  // wave-uniform
-    if (last) seg_geom(data, nxt);
-    uint4 cn[U];
+  // One tile: issue the loads of the next item into cn, then sum c.
+  // Returns true when the wave has no next item.
+  auto step = [&](const uint4 (&c)[U], uint4 (&cn)[U]) __attribute__((always_inline)) -> bool {
+    // the chunk's tiles cover [0, xe] (a point may sit at xe itself)
+    const bool last = t * T + T > cur.xe;  // wave-uniform
+    SegChunk nn;  // the chunk after next: its loads go out before this
+                  // step's tile loads, so waiting on them never waits on those
+    if (last) {
+      seg_geom(data, A.n, nxt);
+      seg_load(A, sp, (ch + 2u * nwave) * 64u, lane, nn);
+    }
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
                           end, cn);
 
@@ -1097,30 +1157,78 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
     bool here = false;
 #pragma unroll
     for (int i = 0; i < 4; ++i) here |= pt[i].x - tb < T;
-    if (__any((int)here)) {  // a packet boundary lies in this tile
+    if (RX) {  // a header window [floor4(start), +24) still being gathered
+      const uint64_t hs = pt[0].x & ~3ull;
+      here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
+    }
+    if (__any((int)here)) {  // a packet boundary (or header) lies in this tile
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         s_data[wid][u * 64 + lane] = c[u];
-        s_pl[wid][u * 64 + lane] = pl[u];
-        if (exact) s_pt[wid][u * 64 + lane] = ptt[u];
+        s_pre[wid][u * 64 + lane] = pl[u];
       }
       __builtin_amdgcn_wave_barrier();
+      if (RX && rx.need) {  // gather header dwords held by this tile, parse
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          const uint64_t q = (pt[0].x & ~3ull) + 4u * (uint32_t)j - tb;
+          if (((rx.need >> j) & 1u) && q < T) {
+            rx.h[j] = s_dw[(uint32_t)q >> 2];
+            rx.need &= ~(1u << j);
+          }
+        }
+        if (rx.need == 0u) {
+          uint32_t hl, tl;
+          rx_parse(rx, (uint32_t)pt[0].x & 3u, pt[1].x - pt[0].x, hl, tl);
+          pt[2].x = pt[0].x + hl;
+          pt[3].x = pt[0].x + tl;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint64_t q = pt[i].x - tb;
         if (q < T) {
           const uint32_t k = (uint32_t)q >> 4;
-          const uint4 d = s_data[wid][k];
-          pt[i].p = s_pl[wid][k] + seg_part<false>(d, (uint32_t)q & 15u);
-          if (exact) pt[i].t = s_pt[wid][k] + seg_part<true>(d, (uint32_t)q & 15u);
+          pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
         }
       }
       __builtin_amdgcn_wave_barrier();
+      if (exact) {  // second pass, same buffer: the byte-sum prefixes
+#pragma unroll
+        for (int u = 0; u < U; ++u) s_pre[wid][u * 64 + lane] = ptt[u];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint64_t q = pt[i].x - tb;
+          if (q < T) {
+            const uint32_t k = (uint32_t)q >> 4;
+            pt[i].t = s_pre[wid][k] + seg_part<true>(s_data[wid][k], (uint32_t)q & 15u);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
     }
 
-    if (last) {
-      if (lane < cur.m) {
-        const uint32_t odd = (uint32_t)pt[0].x & 1u;
+    if (!last) {
+      ++t;
+      return false;
+    }
+    if (cur.p0 + lane < A.n) {
+      const uint32_t odd = (uint32_t)pt[0].x & 1u;
+      if (RX) {
+        // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
+        // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
+        uint32_t r = rx.flags;
+        if (!(r & YU_RX_INVALID)) {
+          const uint32_t ip = fold32(le_to_be(pt[2].p - pt[0].p, odd));
+          if (ip == 0u || ip == 0xFFFFu) r |= YU_RX_IP_OK;
+          if (r & YU_RX_L4) {
+            const uint32_t l4 = fold32(le_to_be(pt[3].p - pt[2].p, odd) + rx.pseudo);
+            if (l4 == 0u || l4 == 0xFFFFu) r |= YU_RX_L4_OK;
+          }
+        }
+        if (A.out) A.out[cur.p0 + lane] = (uint16_t)r;
+      } else {
         uint32_t v;
         if (exact) {
           const uint32_t L = pt[1].p - pt[0].p;
@@ -1135,17 +1243,23 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
         finish_packet(A, cur.p0 + lane, v, len, cur.sd, A.fill ? A.fill + cur.ox : nullptr,
                       (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
       }
-      if (nxt.m == 0) break;
-      cur = nxt;
-      ch += nwave;
-      seg_load(A, sp, (ch + nwave) * 64u, lane, nxt);
-      begin_chunk(cur);
-      t = 0;
-    } else {
-      ++t;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) c[u] = cn[u];
+    if (nxt.p0 >= A.n) return true;
+    cur = nxt;
+    nxt = nn;
+    ch += nwave;
+    begin_chunk(cur);
+    t = 0;
+    return false;
+  };
+
+  // ping-pong: the loads of tile i+1 land in the buffer tile i-1 used, so
+  // no register copy waits on them
+  uint4 ca[U], cb[U];
+  seg_fetch<U, NT != 0>(cur.b0, cur.xe, 0, lane, end, ca);
+  for (;;) {
+    if (step(ca, cb)) break;
+    if (step(cb, ca)) break;
   }
 }
 
@@ -1179,7 +1293,9 @@ const Variant kSmall[] = {
 const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, 0, false>, k_loop<4, 1, false>, k_loop<4, 1, false>}, 64, 1};
 const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, 0, true>, k_loop<4, 1, true>, k_loop<4, 1, true>}, 64, 1};
 const Variant kRag = {"k_rag<16,6>", 1536, {k_rag<16, 6, 0>, k_rag<16, 6, 1>, k_rag<16, 6, 2>}, 16, 4};
-const Variant kSeg = {"k_seg<4>", 0, {k_seg<4, 0>, k_seg<4, 1>, k_seg<4, 2>}, 64, 64};
+const Variant kSeg4 = {"k_seg<4>", 0, {k_seg<4, 0, false>, k_seg<4, 1, false>, k_seg<4, 1, false>}, 64, 64};
+const Variant kSeg8 = {"k_seg<8>", 0, {k_seg<8, 0, false>, k_seg<8, 1, false>, k_seg<8, 1, false>}, 64, 64};
+const Variant kSegRx = {"k_seg<4,rx>", 0, {k_seg<4, 0, true>, k_seg<4, 1, true>, k_seg<4, 1, true>}, 64, 64};
 
 // Ragged kernel choice: the segmented stream sum, except for the IPv4 modes,
 // which read only each packet's header (k_rag's per-packet windows).
@@ -1187,8 +1303,10 @@ const Variant kSeg = {"k_seg<4>", 0, {k_seg<4, 0>, k_seg<4, 1>, k_seg<4, 2>}, 64
 const Variant &pick_ragged(int mode) {
   static const char *f = getenv("YU_RAGGED");
   if (f && strcmp(f, "loop") == 0) return mode == YU_MODE_RAW ? kLoopBE : kLoopLE;
+  if (mode == YU_MODE_VERIFY_RX) return kSegRx;
   if (mode_is_ipv4(mode) || (f && strcmp(f, "rag") == 0)) return kRag;
-  return kSeg;
+  if (f && strcmp(f, "seg8") == 0) return kSeg8;
+  return kSeg4;
 }
 
 // Tuning override (measurement only): YU_VARIANT=<name> forces a k_small
@@ -1211,7 +1329,10 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
   // k_tiny: no junk bytes (4-aligned starts, no TX field, no IPv4 header walk)
   const bool tiny_ok = aligned4 && (mode == YU_MODE_RAW || mode == YU_MODE_VERIFY_TCP ||
                                     mode == YU_MODE_VERIFY_UDP);
+  if (mode == YU_MODE_VERIFY_RX) return kSegRx;
   if (const char *f = forced_variant()) {
+    if (strcmp(f, kSeg4.name) == 0) return kSeg4;
+    if (strcmp(f, kSeg8.name) == 0) return kSeg8;
     for (const Variant &v : kSmall)
       if (strcmp(v.name, f) == 0 && fits(v)) return v;
     for (const Variant &v : kTiny)
