@@ -68,17 +68,22 @@ class Workload:
             nbytes = n * self.L
             self.side = 8 * n  # addrs
             self.name = "config3: 1M x 1500-B TCP segments incl. pseudo-header (sendTCP field value)"
-        elif cfg == 4:  # ragged 64..9000 B, back-to-back, RAW with initial
-            self.mode = batch.RAW
-            rng = np.random.default_rng(4)
-            lens = rng.integers(64, 9001, size=n)
+        elif cfg in (4, 6):
+            # 4: ragged 64..9000 B back-to-back, RAW with initial (BASELINE config 4)
+            # 6: tun RX burst, 1M whole IPv4 datagrams U{40..1500} B, VERIFY_RX (§8f row 1)
+            self.mode = batch.RAW if cfg == 4 else batch.VERIFY_RX
+            rng = np.random.default_rng(cfg)
+            lens = rng.integers(64, 9001, size=n) if cfg == 4 else rng.integers(40, 1501, size=n)
             offs = np.zeros(n + 1, dtype=np.int64)
             offs[1:] = np.cumsum(lens)
             nbytes = int(offs[-1])
             self.L = 0
             self.offsets = torch.from_numpy(offs).to(dev)
-            self.side = 8 * (n + 1) + 2 * n
-            self.name = "config4: ragged 1M packets U{64..9000} B back-to-back (odd offsets), one wave per packet"
+            self.lens = torch.from_numpy(lens).to(dev)
+            self.side = 8 * (n + 1) + (2 * n if cfg == 4 else 0)
+            self.name = ("config4: ragged 1M packets U{64..9000} B back-to-back (odd offsets)" if cfg == 4 else
+                         "tun RX: 1M received IPv4 datagrams U{40..1500} B back-to-back, header + TCP "
+                         "checksum verification (VERIFY_RX)")
         else:
             raise SystemExit(f"unknown config {cfg}")
         self.payload = nbytes
@@ -90,6 +95,12 @@ class Workload:
                 v = d.view(n, self.L)
                 v[:, 12] = 0x50
                 v[:, 16:18] = 0
+            if cfg == 6:  # IPv4 header: IHL 5, TotalLength = packet length, protocol TCP
+                s0 = self.offsets[:-1]
+                d[s0] = 0x45
+                d[s0 + 2] = (self.lens >> 8).to(torch.uint8)
+                d[s0 + 3] = (self.lens & 0xFF).to(torch.uint8)
+                d[s0 + 9] = 6
             self.data.append(d)
         if cfg == 2 or cfg == 4:
             self.initial_arr = torch.randint(0, 65536, (n,), dtype=torch.int32, device=dev,
@@ -114,7 +125,7 @@ class Workload:
 
     def kernel_name(self) -> str:
         if self.offsets is not None:
-            return "k_loop<4,BE>" if self.mode == batch.RAW else "k_loop<4,LE>"
+            return batch.ragged_variant(self.mode)
         return batch.variant(self.L, self.L, self.mode, self.data[0].data_ptr() & 15)
 
 
@@ -231,7 +242,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4])
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 6])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip configs 2/4 side measurements")
     ap.add_argument("--cpu-budget", type=float, default=6.0, help="wall seconds for the CPU baseline")
@@ -290,7 +301,7 @@ def main():
             "workload": w.name,
             "packets_per_gpu": w.n,
             "packet_bytes": w.L if w.L else "U{64..9000}",
-            "mode": {0: "raw", 2: "tcp"}.get(w.mode, str(w.mode)),
+            "mode": {0: "raw", 2: "tcp", 8: "verify_rx"}.get(w.mode, str(w.mode)),
             "algorithmic_bytes_per_step_per_gpu": w.bytes,
             "rotating_batches": w.R,
             "kernel": w.kernel_name(),
@@ -311,7 +322,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_extra:
         extra = {}
-        for c in (2, 3, 4):
+        for c in (2, 3, 4, 6):
             if c == args.config:
                 continue
             wc = Workload(c, dev, seed=77 + c)

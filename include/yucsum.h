@@ -113,7 +113,7 @@ uint16_t yu_pseudo_header_checksum(uint32_t protocol,
  * network/ipv4/icmp.go:36-45. initial and addrs are ignored. */
 #define YU_MODE_ICMP 4
 /* Receive-side verification, checker semantics (checker/checker.go:25-40):
- * out[i] = Checksum(b[:IHL*4], 0) INCLUDING the stored field. The packet is
+ * out[i] = Checksum(b[:IHL*4] clamped to len, 0) INCLUDING the stored field. The packet is
  * valid iff out[i] is 0x0000 or 0xFFFF. */
 #define YU_MODE_VERIFY_IPV4 5
 /* checker.TCP (checker/checker.go:71-99): out[i] = Checksum over
@@ -214,6 +214,32 @@ int yu_csum_batch_host_uniform(const uint8_t *h_data, uint64_t stride,
                                uint16_t initial, const uint8_t *h_addrs,
                                uint16_t *h_out, int device);
 
+/* The same for a ragged host batch: packet i = h_data[h_offsets[i],
+ * h_offsets[i+1]) (a tun read burst packed back to back). The offsets are
+ * host memory and are validated here (non-decreasing, packet lengths within
+ * the mode's limit), then shipped rebased with each slice. */
+int yu_csum_batch_host_ragged(const uint8_t *h_data, const uint64_t *h_offsets,
+                              uint64_t n, int mode,
+                              const uint16_t *h_initial_arr, uint16_t initial,
+                              const uint8_t *h_addrs, uint16_t *h_out,
+                              int device);
+
+/* Scatter-gather packets, as the tun endpoint reads them into several views
+ * (link/tundev/tundev.go:116-125; buffer.VectorisedView, buffer/view.go:
+ * 37-46): packet i is the concatenation of iov[first_iov[i]] ..
+ * iov[first_iov[i+1] - 1]. The views are gathered into the library's pinned
+ * staging while earlier slices are on the GPU. Layout-compatible with
+ * struct iovec. */
+typedef struct yu_iovec {
+  const void *base;
+  uint64_t len;
+} yu_iovec;
+
+int yu_csum_batch_host_iov(const yu_iovec *iov, const uint64_t *first_iov,
+                           uint64_t n, int mode, const uint16_t *h_initial_arr,
+                           uint16_t initial, const uint8_t *h_addrs,
+                           uint16_t *h_out, int device);
+
 /* ------------------------------------------------------------------ */
 /* Introspection.                                                      */
 /* ------------------------------------------------------------------ */
@@ -225,6 +251,9 @@ int yu_device_count(void);
  * (for profiling and tests; no device needed). Returns a static string. */
 const char *yu_uniform_variant(uint64_t stride, uint32_t len, int mode,
                                uint64_t data_align16);
+/* Name of the kernel variant the ragged path launches for this mode (static
+ * string; "" for a bad mode). */
+const char *yu_ragged_variant(int mode);
 
 #ifdef __cplusplus
 }

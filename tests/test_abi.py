@@ -67,6 +67,14 @@ def test_batched_entry_points_fail_without_gpu():
     assert rc == _lib.YU_ENODEV
     rc = L.yu_csum_batch_host_uniform(ctypes.addressof(buf), 16, 16, 4, 0, None, 0, None, ctypes.addressof(out), 0)
     assert rc == _lib.YU_ENODEV
+    rc = L.yu_csum_batch_host_ragged(ctypes.addressof(buf), ctypes.addressof(offs), 4, 0, None, 0, None,
+                                     ctypes.addressof(out), 0)
+    assert rc == _lib.YU_ENODEV
+    iov = (_lib.YuIovec * 4)(*[_lib.YuIovec(ctypes.addressof(buf) + 16 * i, 16) for i in range(4)])
+    first = (ctypes.c_uint64 * 5)(0, 1, 2, 3, 4)
+    rc = L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 4, 8, None, 0, None,
+                                  ctypes.addressof(out), 0)
+    assert rc == _lib.YU_ENODEV
 
 
 def test_argument_validation_precedes_device():
@@ -84,6 +92,17 @@ def test_argument_validation_precedes_device():
     assert L.yu_csum_fill_uniform(p + 1, 16, 16, 4, 1, None, 0, None, o, None) == _lib.YU_EINVAL  # unaligned
     assert L.yu_csum_batch_ragged(p, None, 4, 0, None, 0, None, o, None) == _lib.YU_EINVAL
     assert L.yu_csum_batch_host_uniform(p, 16, 16, 4, 99, None, 0, None, o, 0) == _lib.YU_EINVAL
+    # host ragged / iov: offsets and views are host memory, checked before any device work
+    bad = (ctypes.c_uint64 * 5)(0, 16, 8, 48, 64)  # decreasing
+    assert L.yu_csum_batch_host_ragged(p, ctypes.addressof(bad), 4, 0, None, 0, None, o, 0) == _lib.YU_EINVAL
+    big = (ctypes.c_uint64 * 2)(0, 70000)  # > 65535 in a transport mode
+    assert L.yu_csum_batch_host_ragged(p, ctypes.addressof(big), 1, 2, None, 0, None, o, 0) == _lib.YU_EINVAL
+    iov = (_lib.YuIovec * 2)(_lib.YuIovec(None, 5), _lib.YuIovec(p, 4))  # NULL view with bytes
+    first = (ctypes.c_uint64 * 2)(0, 2)
+    assert L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 1, 0, None, 0, None,
+                                    o, 0) == _lib.YU_EINVAL
+    assert L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 1, 9, None, 0, None,
+                                    o, 0) == _lib.YU_EINVAL  # mode
 
 
 def test_python_front_end_refuses_cpu_tensors():

@@ -314,6 +314,36 @@ def test_host_uniform_path(dev, oracle_c):
     assert np.array_equal(got, want)
 
 
+def test_host_ragged_and_iov_paths(dev, oracle_c):
+    """Host-memory ragged bursts and scatter-gather packets (tundev's 4-view readv,
+    link/tundev/tundev.go:116-125) through the pinned pipeline, against the oracle."""
+    import rxgen
+    rng = np.random.default_rng(23)
+    lens = rng.integers(0, 9001, size=20000)
+    lens[::997] = 40 << 20  # a few packets longer than a 32 MiB slice
+    offs = np.zeros(lens.size + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    offs += 3
+    blob = _rand(rng, int(offs[-1]) + 5)
+    init = rng.integers(0, 65536, size=lens.size, dtype=np.uint16)
+    got = batch.checksum_host_ragged(blob, offs, "raw", initial_arr=init)
+    want = oracle_c.batch(blob, O.MODE_RAW, offsets=offs, initial_arr=init, threads=8)
+    assert np.array_equal(got, want)
+    # RX datagrams split at the tun view boundaries 128/384/896 (tundev.go:20)
+    rblob, roffs = rxgen.rx_batch(rng, 4000, lo=0, hi=1480)
+    want = oracle_c.batch(rblob, O.MODE_VERIFY_RX, offsets=roffs)
+    got = batch.checksum_host_ragged(rblob, roffs, "verify_rx")
+    assert np.array_equal(got, want)
+    cuts = [128, 128 + 384, 128 + 384 + 896]
+    pkts = []
+    for i in range(roffs.size - 1):
+        pk = rblob[int(roffs[i]):int(roffs[i + 1])]
+        edges = [0] + [c for c in cuts if c < pk.size] + [pk.size]
+        pkts.append([pk[a:b] for a, b in zip(edges[:-1], edges[1:])])
+    got = batch.checksum_host_iov(pkts, "verify_rx")
+    assert np.array_equal(got, want)
+
+
 def test_errors_are_loud(dev):
     from yustack_amd._lib import YuError
     d = torch.zeros(1 << 17, dtype=torch.uint8, device=dev)

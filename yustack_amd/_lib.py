@@ -17,11 +17,17 @@ EXPORTS = (
     "yu_checksum", "yu_checksum_combine", "yu_pseudo_header_checksum",
     "yu_csum_batch_uniform", "yu_csum_batch_ragged",
     "yu_csum_fill_uniform", "yu_csum_fill_ragged",
-    "yu_csum_batch_host_uniform",
+    "yu_csum_batch_host_uniform", "yu_csum_batch_host_ragged", "yu_csum_batch_host_iov",
     "yu_abi_version", "yu_strerror", "yu_device_count", "yu_uniform_variant",
+    "yu_ragged_variant",
 )
 
 YU_OK, YU_EINVAL, YU_ENODEV, YU_ENOMEM, YU_EHIP_BASE = 0, -22, -19, -12, -1000
+
+
+class YuIovec(ctypes.Structure):
+    """struct yu_iovec (include/yucsum.h): one view of a scatter-gather packet."""
+    _fields_ = [("base", ctypes.c_void_p), ("len", ctypes.c_uint64)]
 
 
 class YuError(RuntimeError):
@@ -61,6 +67,10 @@ def lib() -> ctypes.CDLL:
         f.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, vp]
     L.yu_csum_batch_host_uniform.restype = i32
     L.yu_csum_batch_host_uniform.argtypes = [vp, u64, u32, u64, i32, vp, u16, vp, vp, i32]
+    L.yu_csum_batch_host_ragged.restype = i32
+    L.yu_csum_batch_host_ragged.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, i32]
+    L.yu_csum_batch_host_iov.restype = i32
+    L.yu_csum_batch_host_iov.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, i32]
     L.yu_abi_version.restype = i32
     L.yu_abi_version.argtypes = []
     L.yu_strerror.restype = c.c_char_p
@@ -69,6 +79,8 @@ def lib() -> ctypes.CDLL:
     L.yu_device_count.argtypes = []
     L.yu_uniform_variant.restype = c.c_char_p
     L.yu_uniform_variant.argtypes = [u64, u32, i32, u64]
+    L.yu_ragged_variant.restype = c.c_char_p
+    L.yu_ragged_variant.argtypes = [i32]
     del u8
     _lib = L
     return L

@@ -179,6 +179,76 @@ def checksum_host_uniform(data: np.ndarray, stride: int, length: int, n: int, mo
     return out
 
 
+def _host_side(n, initial_arr, addrs, out):
+    ia = None if initial_arr is None else np.ascontiguousarray(initial_arr, dtype=np.uint16)
+    ad = None if addrs is None else np.ascontiguousarray(addrs, dtype=np.uint8)
+    if ia is not None and ia.size < n or ad is not None and ad.size < 8 * n:
+        raise ValueError("side arrays too small")
+    if out is None:
+        out = np.empty(n, dtype=np.uint16)
+    elif out.dtype != np.uint16 or out.size < n or not out.flags.c_contiguous:
+        raise ValueError("out must be a contiguous uint16 array of >= n elements")
+    return ia, ad, out
+
+
+def checksum_host_ragged(data, offsets, mode="raw", *, initial: int = 0, initial_arr=None,
+                         addrs=None, out: np.ndarray | None = None, device: int = 0) -> np.ndarray:
+    """Ragged host batch (packet i = data[offsets[i]:offsets[i+1]], e.g. a tun read
+    burst) through the pinned, pipelined host path (yu_csum_batch_host_ragged)."""
+    m = _mode(mode)
+    if isinstance(data, torch.Tensor):
+        if data.is_cuda or data.dtype != torch.uint8 or not data.is_contiguous():
+            raise TypeError("data must be a contiguous uint8 CPU tensor")
+        dptr, dlen = data.data_ptr(), data.numel()
+    else:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        dptr, dlen = data.ctypes.data, data.size
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offs.size - 1
+    if n < 0:
+        raise ValueError("offsets must hold n+1 entries")
+    if n and int(offs[-1]) > dlen:
+        raise ValueError("offsets run past data")
+    ia, ad, out = _host_side(n, initial_arr, addrs, out)
+    rc = lib().yu_csum_batch_host_ragged(dptr, offs.ctypes.data, n, m,
+                                         None if ia is None else ia.ctypes.data, initial & 0xFFFF,
+                                         None if ad is None else ad.ctypes.data, out.ctypes.data, device)
+    check(rc, "yu_csum_batch_host_ragged")
+    return out
+
+
+def checksum_host_iov(packets, mode="raw", *, initial: int = 0, initial_arr=None, addrs=None,
+                      out: np.ndarray | None = None, device: int = 0) -> np.ndarray:
+    """Scatter-gather host packets: ``packets[i]`` is a list of views (numpy uint8
+    arrays / bytes) whose concatenation is packet i, as tundev's readv fills them
+    (link/tundev/tundev.go:116-125). Gathered into pinned staging by the library."""
+    from ._lib import YuIovec
+    m = _mode(mode)
+    n = len(packets)
+    keep, views = [], []
+    first = np.zeros(n + 1, np.uint64)
+    for i, pk in enumerate(packets):
+        for v in pk:
+            a = np.frombuffer(v, np.uint8) if isinstance(v, (bytes, bytearray)) else \
+                np.ascontiguousarray(v, dtype=np.uint8)
+            keep.append(a)
+            views.append((a.ctypes.data if a.size else None, a.size))
+        first[i + 1] = len(views)
+    iov = (YuIovec * max(1, len(views)))(*[YuIovec(b, l) for b, l in views])
+    ia, ad, out = _host_side(n, initial_arr, addrs, out)
+    rc = lib().yu_csum_batch_host_iov(ctypes_addr(iov), first.ctypes.data, n, m,
+                                      None if ia is None else ia.ctypes.data, initial & 0xFFFF,
+                                      None if ad is None else ad.ctypes.data, out.ctypes.data, device)
+    del keep
+    check(rc, "yu_csum_batch_host_iov")
+    return out
+
+
+def ctypes_addr(obj) -> int:
+    import ctypes
+    return ctypes.addressof(obj)
+
+
 def verified(sums: torch.Tensor) -> torch.Tensor:
     """checker semantics: a VERIFY_* sum is valid iff it is 0x0000 or 0xFFFF."""
     s = sums.view(torch.int16)
@@ -192,6 +262,11 @@ def rx_accepted(flags: torch.Tensor) -> torch.Tensor:
     ok_ip = (f & (RX_IP_OK | RX_INVALID)) == RX_IP_OK
     ok_l4 = ((f & RX_L4) == 0) | ((f & RX_L4_OK) != 0)
     return ok_ip & ok_l4
+
+
+def ragged_variant(mode="raw") -> str:
+    """Name of the kernel the ragged path launches for this mode."""
+    return lib().yu_ragged_variant(_mode(mode)).decode()
 
 
 def variant(stride: int, length: int, mode="raw", align16: int = 0) -> str:

@@ -1,4 +1,5 @@
-// yucsum_host.cpp — host-memory batched entry point (yu_csum_batch_host_uniform).
+// yucsum_host.cpp — host-memory batched entry points
+// (yu_csum_batch_host_uniform / _ragged / _iov).
 //
 // yustack's packets start and end in host memory: the tun link endpoint
 // reads into Go slices (link/tundev/tundev.go:78-151) and writes them back
@@ -10,9 +11,12 @@
 //
 // on one of three staging slots, each with its own stream, so the H2D of
 // slice k+1, the kernel of slice k and the D2H of slice k-1 overlap, and
-// the CPU staging copy of the next slice overlaps all of them. Staging
-// buffers are per (calling thread, device) and grow on demand; nothing is
-// shared between threads, so concurrent callers need no lock.
+// the CPU staging copy of the next slice overlaps all of them. Slices are
+// whole packets, about 32 MiB each. Ragged batches ship rebased offsets with
+// each slice; scatter-gather (iovec) packets are gathered into the staging
+// slot while the previous slices are on the GPU. Staging buffers are per
+// (calling thread, device) and grow on demand; nothing is shared between
+// threads, so concurrent callers need no lock.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -43,8 +47,10 @@ int hip_rc(hipError_t e) {
 struct Slot {
   uint8_t *h_data = nullptr, *h_addrs = nullptr;
   uint16_t *h_init = nullptr, *h_out = nullptr;
+  uint64_t *h_off = nullptr;
   uint8_t *d_data = nullptr, *d_addrs = nullptr;
   uint16_t *d_init = nullptr, *d_out = nullptr;
+  uint64_t *d_off = nullptr;
   hipStream_t st = nullptr;
   hipEvent_t done = nullptr;
   uint64_t first = 0, cnt = 0;
@@ -62,10 +68,12 @@ struct Ctx {
       if (x.h_addrs) (void)hipHostFree(x.h_addrs);
       if (x.h_init) (void)hipHostFree(x.h_init);
       if (x.h_out) (void)hipHostFree(x.h_out);
+      if (x.h_off) (void)hipHostFree(x.h_off);
       if (x.d_data) (void)hipFree(x.d_data);
       if (x.d_addrs) (void)hipFree(x.d_addrs);
       if (x.d_init) (void)hipFree(x.d_init);
       if (x.d_out) (void)hipFree(x.d_out);
+      if (x.d_off) (void)hipFree(x.d_off);
       if (x.done) (void)hipEventDestroy(x.done);
       if (x.st) (void)hipStreamDestroy(x.st);
       x = Slot();
@@ -78,6 +86,8 @@ struct Ctx {
 
   int reserve(uint64_t data_bytes, uint64_t pk) {
     if (data_bytes <= cap_data && pk <= cap_pk) return YU_OK;
+    if (data_bytes < cap_data) data_bytes = cap_data;
+    if (pk < cap_pk) pk = cap_pk;
     release();
     for (Slot &x : s) {
       YU_TRY(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
@@ -86,10 +96,12 @@ struct Ctx {
       YU_TRY(hipHostMalloc((void **)&x.h_addrs, pk * 8, 0));
       YU_TRY(hipHostMalloc((void **)&x.h_init, pk * 2, 0));
       YU_TRY(hipHostMalloc((void **)&x.h_out, pk * 2, 0));
+      YU_TRY(hipHostMalloc((void **)&x.h_off, (pk + 1) * 8, 0));
       YU_TRY(hipMalloc((void **)&x.d_data, data_bytes ? data_bytes : 16));
       YU_TRY(hipMalloc((void **)&x.d_addrs, pk * 8));
       YU_TRY(hipMalloc((void **)&x.d_init, pk * 2));
       YU_TRY(hipMalloc((void **)&x.d_out, pk * 2));
+      YU_TRY(hipMalloc((void **)&x.d_off, (pk + 1) * 8));
     }
     cap_data = data_bytes;
     cap_pk = pk;
@@ -116,9 +128,7 @@ int finish(Slot &x, uint16_t *h_out) {
   return YU_OK;
 }
 
-int run(const uint8_t *h_data, uint64_t stride, uint32_t len, uint64_t n,
-        int mode, const uint16_t *h_init, uint16_t initial,
-        const uint8_t *h_addrs, uint16_t *h_out, int device) {
+Ctx &context(int device) {
   std::unique_ptr<Ctx> &cp = t_ctx[device];
   if (!cp) {
     cp.reset(new Ctx());
@@ -131,29 +141,39 @@ int run(const uint8_t *h_data, uint64_t stride, uint32_t len, uint64_t n,
     if (x.busy) (void)hipEventSynchronize(x.done);
     x.busy = false;
   }
-  const uint64_t pstride = stride ? stride : 1;
-  uint64_t slice = kSliceBytes / pstride;
-  if (slice < 1) slice = 1;
-  if (slice > n) slice = n;
-  const uint64_t data_bytes = (slice - 1) * stride + len;
-  int rc = c.reserve(data_bytes, slice);
-  if (rc) return rc;
+  return c;
+}
 
-  const bool pin_in = is_pinned(h_data);
+// The slice pipeline shared by the layouts. A Layout says how many packets
+// the slice starting at `first` holds (byte-bounded), how many bytes they
+// span, how to stage them (returning the host pointer the H2D copy reads:
+// the caller's pinned buffer or the slot's staging), and how to launch.
+template <class Layout>
+int pipeline(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
+             const uint8_t *h_addrs, uint16_t *h_out) {
+  // capacity: the largest slice of this batch
+  uint64_t max_b = 0, max_pk = 0;
+  for (uint64_t first = 0; first < n;) {
+    const uint64_t cnt = L.count(first);
+    const uint64_t b = L.bytes(first, cnt);
+    if (b > max_b) max_b = b;
+    if (cnt > max_pk) max_pk = cnt;
+    first += cnt;
+  }
+  int rc = c.reserve(max_b, max_pk);
+  if (rc) return rc;
   const bool pin_out = is_pinned(h_out);
   uint64_t k = 0;
-  for (uint64_t first = 0; first < n; first += slice, ++k) {
+  for (uint64_t first = 0; first < n; ++k) {
     Slot &x = c.s[k % kSlots];
     rc = finish(x, h_out);
     if (rc) return rc;
-    const uint64_t cnt = (n - first) < slice ? (n - first) : slice;
-    const uint64_t bytes = (cnt - 1) * stride + len;
-    const uint8_t *src = h_data + first * stride;
-    if (!pin_in && bytes) {
-      memcpy(x.h_data, src, bytes);
-      src = x.h_data;
-    }
+    const uint64_t cnt = L.count(first);
+    const uint64_t bytes = L.bytes(first, cnt);
+    const uint8_t *src = L.stage(x, first, cnt);
     if (bytes) YU_TRY(hipMemcpyAsync(x.d_data, src, bytes, hipMemcpyHostToDevice, x.st));
+    if (L.ragged())
+      YU_TRY(hipMemcpyAsync(x.d_off, x.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice, x.st));
     const uint16_t *d_init = nullptr;
     const uint8_t *d_addrs = nullptr;
     if (h_init) {
@@ -166,8 +186,7 @@ int run(const uint8_t *h_data, uint64_t stride, uint32_t len, uint64_t n,
       YU_TRY(hipMemcpyAsync(x.d_addrs, x.h_addrs, cnt * 8, hipMemcpyHostToDevice, x.st));
       d_addrs = x.d_addrs;
     }
-    rc = yu_csum_batch_uniform(x.d_data, stride, len, cnt, mode, d_init,
-                               initial, d_addrs, x.d_out, x.st);
+    rc = L.launch(x, cnt, d_init, d_addrs);
     if (rc) return rc;
     x.staged_out = !pin_out;
     YU_TRY(hipMemcpyAsync(pin_out ? h_out + first : x.h_out, x.d_out, cnt * 2,
@@ -176,6 +195,7 @@ int run(const uint8_t *h_data, uint64_t stride, uint32_t len, uint64_t n,
     x.first = first;
     x.cnt = cnt;
     x.busy = true;
+    first += cnt;
   }
   for (Slot &x : c.s) {
     rc = finish(x, h_out);
@@ -183,6 +203,128 @@ int run(const uint8_t *h_data, uint64_t stride, uint32_t len, uint64_t n,
   }
   return YU_OK;
 }
+
+// packet i = data[i*stride, i*stride + len)
+struct UniformLayout {
+  const uint8_t *h_data;
+  uint64_t stride, n, slice;
+  uint32_t len;
+  int mode;
+  uint16_t initial;
+  bool pin_in;
+  bool ragged() const { return false; }
+  uint64_t count(uint64_t first) const { return n - first < slice ? n - first : slice; }
+  uint64_t bytes(uint64_t, uint64_t cnt) const { return (cnt - 1) * stride + len; }
+  const uint8_t *stage(Slot &x, uint64_t first, uint64_t cnt) const {
+    const uint8_t *src = h_data + first * stride;
+    const uint64_t b = bytes(first, cnt);
+    if (pin_in || !b) return src;
+    memcpy(x.h_data, src, b);
+    return x.h_data;
+  }
+  int launch(Slot &x, uint64_t cnt, const uint16_t *d_init, const uint8_t *d_addrs) const {
+    return yu_csum_batch_uniform(x.d_data, stride, len, cnt, mode, d_init, initial, d_addrs,
+                                 x.d_out, x.st);
+  }
+};
+
+// Slices of whole packets, each up to kSliceBytes (a longer packet is a
+// slice of its own); `span(i)` = bytes of packet i.
+template <class Span>
+uint64_t byte_slice(uint64_t first, uint64_t n, const Span &span) {
+  uint64_t cnt = 0, b = 0;
+  while (first + cnt < n) {
+    const uint64_t l = span(first + cnt);
+    if (cnt && b + l > kSliceBytes) break;
+    b += l;
+    ++cnt;
+  }
+  return cnt;
+}
+
+// packet i = data[off[i], off[i+1]) (tun burst, back to back)
+struct RaggedLayout {
+  const uint8_t *h_data;
+  const uint64_t *off;
+  uint64_t n;
+  int mode;
+  uint16_t initial;
+  bool pin_in;
+  bool ragged() const { return true; }
+  uint64_t count(uint64_t first) const {
+    return byte_slice(first, n, [&](uint64_t i) { return off[i + 1] - off[i]; });
+  }
+  uint64_t bytes(uint64_t first, uint64_t cnt) const { return off[first + cnt] - off[first]; }
+  const uint8_t *stage(Slot &x, uint64_t first, uint64_t cnt) const {
+    const uint64_t o0 = off[first];
+    for (uint64_t i = 0; i <= cnt; ++i) x.h_off[i] = off[first + i] - o0;
+    const uint64_t b = bytes(first, cnt);
+    if (pin_in || !b) return h_data + o0;
+    memcpy(x.h_data, h_data + o0, b);
+    return x.h_data;
+  }
+  int launch(Slot &x, uint64_t cnt, const uint16_t *d_init, const uint8_t *d_addrs) const {
+    return yu_csum_batch_ragged(x.d_data, x.d_off, cnt, mode, d_init, initial, d_addrs, x.d_out,
+                                x.st);
+  }
+};
+
+// packet i = iov[first_iov[i]] ‖ ... ‖ iov[first_iov[i+1] - 1], gathered
+// into the staging slot (the tun endpoint's readv into 4 views,
+// link/tundev/tundev.go:116-125, buffer/view.go:37-46)
+struct IovLayout {
+  const yu_iovec *iov;
+  const uint64_t *first_iov;
+  uint64_t n;
+  int mode;
+  uint16_t initial;
+  bool ragged() const { return true; }
+  uint64_t plen(uint64_t i) const {
+    uint64_t l = 0;
+    for (uint64_t v = first_iov[i]; v < first_iov[i + 1]; ++v) l += iov[v].len;
+    return l;
+  }
+  uint64_t count(uint64_t first) const {
+    return byte_slice(first, n, [&](uint64_t i) { return plen(i); });
+  }
+  uint64_t bytes(uint64_t first, uint64_t cnt) const {
+    uint64_t b = 0;
+    for (uint64_t i = first; i < first + cnt; ++i) b += plen(i);
+    return b;
+  }
+  const uint8_t *stage(Slot &x, uint64_t first, uint64_t cnt) const {
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < cnt; ++i) {
+      x.h_off[i] = o;
+      for (uint64_t v = first_iov[first + i]; v < first_iov[first + i + 1]; ++v) {
+        if (iov[v].len) memcpy(x.h_data + o, iov[v].base, iov[v].len);
+        o += iov[v].len;
+      }
+    }
+    x.h_off[cnt] = o;
+    return x.h_data;
+  }
+  int launch(Slot &x, uint64_t cnt, const uint16_t *d_init, const uint8_t *d_addrs) const {
+    return yu_csum_batch_ragged(x.d_data, x.d_off, cnt, mode, d_init, initial, d_addrs, x.d_out,
+                                x.st);
+  }
+};
+
+// Device selection around one call; the caller's current device is restored.
+template <class F>
+int on_device(int device, F &&f) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return YU_ENODEV;
+  if (device < 0 || device >= ndev || device >= 64) return YU_ENODEV;
+  int prev = 0;
+  YU_TRY(hipGetDevice(&prev));
+  YU_TRY(hipSetDevice(device));
+  int rc = f(context(device));
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+bool bad_mode(int mode) { return mode < 0 || mode >= YU_MODE_COUNT; }
 
 }  // namespace
 
@@ -193,18 +335,60 @@ extern "C" int yu_csum_batch_host_uniform(const uint8_t *h_data,
                                           uint16_t initial,
                                           const uint8_t *h_addrs,
                                           uint16_t *h_out, int device) {
-  if (mode < 0 || mode >= YU_MODE_COUNT || !h_out) return YU_EINVAL;
+  if (bad_mode(mode) || !h_out) return YU_EINVAL;
   if (n == 0) return YU_OK;
   if (!h_data && len) return YU_EINVAL;
   if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return YU_ENODEV;
-  if (device < 0 || device >= ndev || device >= 64) return YU_ENODEV;
-  int prev = 0;
-  YU_TRY(hipGetDevice(&prev));
-  YU_TRY(hipSetDevice(device));
-  int rc = run(h_data, stride, len, n, mode, h_initial_arr, initial, h_addrs,
-               h_out, device);
-  (void)hipSetDevice(prev);
-  return rc;
+  if (len > YU_MAX_RAW_LEN) return YU_EINVAL;
+  return on_device(device, [&](Ctx &c) {
+    const uint64_t pstride = stride ? stride : 1;
+    uint64_t slice = kSliceBytes / pstride;
+    if (slice < 1) slice = 1;
+    if (slice > n) slice = n;
+    UniformLayout L{h_data, stride, n, slice, len, mode, initial, is_pinned(h_data)};
+    return pipeline(c, L, n, h_initial_arr, h_addrs, h_out);
+  });
+}
+
+extern "C" int yu_csum_batch_host_ragged(const uint8_t *h_data,
+                                         const uint64_t *h_offsets, uint64_t n,
+                                         int mode, const uint16_t *h_initial_arr,
+                                         uint16_t initial,
+                                         const uint8_t *h_addrs,
+                                         uint16_t *h_out, int device) {
+  if (bad_mode(mode) || !h_out) return YU_EINVAL;
+  if (n == 0) return YU_OK;
+  if (!h_offsets || (!h_data && h_offsets[n] != h_offsets[0])) return YU_EINVAL;
+  const uint64_t cap = mode == YU_MODE_RAW ? YU_MAX_RAW_LEN : YU_MAX_TRANSPORT_LEN;
+  for (uint64_t i = 0; i < n; ++i)  // host offsets: checked here, unlike the device call
+    if (h_offsets[i + 1] < h_offsets[i] || h_offsets[i + 1] - h_offsets[i] > cap)
+      return YU_EINVAL;
+  return on_device(device, [&](Ctx &c) {
+    RaggedLayout L{h_data, h_offsets, n, mode, initial, is_pinned(h_data)};
+    return pipeline(c, L, n, h_initial_arr, h_addrs, h_out);
+  });
+}
+
+extern "C" int yu_csum_batch_host_iov(const yu_iovec *iov,
+                                      const uint64_t *first_iov, uint64_t n,
+                                      int mode, const uint16_t *h_initial_arr,
+                                      uint16_t initial, const uint8_t *h_addrs,
+                                      uint16_t *h_out, int device) {
+  if (bad_mode(mode) || !h_out) return YU_EINVAL;
+  if (n == 0) return YU_OK;
+  if (!first_iov || (!iov && first_iov[n] != first_iov[0])) return YU_EINVAL;
+  const uint64_t cap = mode == YU_MODE_RAW ? YU_MAX_RAW_LEN : YU_MAX_TRANSPORT_LEN;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (first_iov[i + 1] < first_iov[i]) return YU_EINVAL;
+    uint64_t l = 0;
+    for (uint64_t v = first_iov[i]; v < first_iov[i + 1]; ++v) {
+      if (!iov[v].base && iov[v].len) return YU_EINVAL;
+      l += iov[v].len;
+    }
+    if (l > cap) return YU_EINVAL;
+  }
+  return on_device(device, [&](Ctx &c) {
+    IovLayout L{iov, first_iov, n, mode, initial};
+    return pipeline(c, L, n, h_initial_arr, h_addrs, h_out);
+  });
 }

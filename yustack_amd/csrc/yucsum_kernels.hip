@@ -936,7 +936,6 @@ __global__ __launch_bounds__(256) void k_rag(BatchArgs A) {
 constexpr uint32_t kInv255 = 0xFEFEFEFFu;  // 255 * kInv255 == 1 (mod 2^32)
 
 struct SegChunk {
-  uint64_t p0;      // first packet of the chunk
   uint64_t ox, oy;  // this lane's packet [ox, oy) as offsets into data (lanes
                     // past the batch: the chunk end)
   uint64_t b0;      // floor4 address of the chunk's first byte (wave-uniform)
@@ -951,7 +950,6 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
                                          uint64_t p0, uint32_t lane, SegChunk &k) {
   const uint64_t n = A.n;
   const uint64_t i = p0 + lane;
-  k.p0 = p0;
   // ragged: two (clamped) offset loads; uniform: arithmetic, with lanes past
   // the batch at the chunk's end (its last packet's end)
   const uint64_t last = p0 < n ? (n - p0 < 64u ? n : p0 + 64u) - 1u : 0u;
@@ -961,9 +959,7 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
   const uint64_t rx = offs[A.offsets ? (i < n ? i : n) : 0];
   k.ox = A.offsets ? rx : (i < n ? i * A.stride : uy);
   k.oy = A.offsets ? ry : uy;
-  k.sd = load_side(sp, i < n ? i : n - 1);
-  k.b0 = (uint64_t)(uintptr_t)A.data & ~3ull;  // set by seg_geom
-  k.xe = 0;
+  k.sd = load_side(sp, i < n ? i : n - 1);  // b0/xe: seg_geom
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
@@ -971,9 +967,14 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
 }
 
-// Wave-uniform geometry of a loaded chunk (waits for its offsets).
-__device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, SegChunk &k) {
-  if (k.p0 >= n) return;  // no such chunk
+// Wave-uniform geometry of a loaded chunk starting at packet p0 (waits for
+// its offsets). No such chunk: an empty range, so its loads are all masked.
+__device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk &k) {
+  if (p0 >= n) {
+    k.b0 = data & ~3ull;
+    k.xe = 0;
+    return;
+  }
   const uint64_t s = data + readlane64(k.ox, 0);
   const uint64_t e = data + readlane64(k.oy, 63);  // lane 63's end = the chunk end
   k.b0 = s & ~3ull;
@@ -1084,7 +1085,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   SegChunk cur, nxt;
   seg_load(A, sp, ch * 64u, lane, cur);
   seg_load(A, sp, (ch + nwave) * 64u, lane, nxt);
-  seg_geom(data, A.n, cur);
+  seg_geom(data, A.n, ch * 64u, cur);
 
   // per-chunk state
   SegPt pt[4];  // start, end, then field start/end (TX) or header/transport end (RX)
@@ -1121,12 +1122,13 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   // One tile: issue the loads of the next item into cn, then sum c.
   // Returns true when the wave has no next item.
   auto step = [&](const uint4 (&c)[U], uint4 (&cn)[U]) __attribute__((always_inline)) -> bool {
-    // the chunk's tiles cover [0, xe] (a point may sit at xe itself)
-    const bool last = t * T + T > cur.xe;  // wave-uniform
+    // the chunk's tiles cover [0, xe); a point at a tile's end (xe itself,
+    // when tile-aligned) takes the running sums after that tile
+    const bool last = t * T + T >= cur.xe;  // wave-uniform
     SegChunk nn;  // the chunk after next: its loads go out before this
                   // step's tile loads, so waiting on them never waits on those
     if (last) {
-      seg_geom(data, A.n, nxt);
+      seg_geom(data, A.n, (ch + nwave) * 64u, nxt);
       seg_load(A, sp, (ch + 2u * nwave) * 64u, lane, nn);
     }
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
@@ -1208,12 +1210,21 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
         __builtin_amdgcn_wave_barrier();
       }
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (pt[i].x - tb == T) pt[i].p = carry_l;
+    if (exact) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (pt[i].x - tb == T) pt[i].t = carry_t;
+    }
 
     if (!last) {
       ++t;
       return false;
     }
-    if (cur.p0 + lane < A.n) {
+    const uint64_t p = ch * 64u + lane;
+    if (p < A.n) {
       const uint32_t odd = (uint32_t)pt[0].x & 1u;
       if (RX) {
         // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
@@ -1227,7 +1238,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
             if (l4 == 0u || l4 == 0xFFFFu) r |= YU_RX_L4_OK;
           }
         }
-        if (A.out) A.out[cur.p0 + lane] = (uint16_t)r;
+        if (A.out) A.out[p] = (uint16_t)r;
       } else {
         uint32_t v;
         if (exact) {
@@ -1240,11 +1251,11 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
           v = le_to_be(pt[1].p - pt[0].p - (pt[3].p - pt[2].p), odd);
         }
         const uint64_t len = pt[1].x - pt[0].x;
-        finish_packet(A, cur.p0 + lane, v, len, cur.sd, A.fill ? A.fill + cur.ox : nullptr,
+        finish_packet(A, p, v, len, cur.sd, A.fill ? A.fill + cur.ox : nullptr,
                       (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
       }
     }
-    if (nxt.p0 >= A.n) return true;
+    if ((ch + nwave) * 64u >= A.n) return true;
     cur = nxt;
     nxt = nn;
     ch += nwave;
@@ -1528,6 +1539,11 @@ int yu_csum_fill_ragged(uint8_t *data, const uint64_t *offsets, uint64_t n,
 const char *yu_uniform_variant(uint64_t stride, uint32_t len, int mode,
                                uint64_t data_align16) {
   return pick_uniform(data_align16 & 15u, stride, len, 2, mode).name;
+}
+
+const char *yu_ragged_variant(int mode) {
+  if (mode < 0 || mode >= YU_MODE_COUNT) return "";
+  return pick_ragged(mode).name;
 }
 
 int yu_device_count(void) {
