@@ -31,6 +31,10 @@ def short_name(full):
         return f"k_tiny<{args[0]}>"
     if k == "k_loop":
         return f"k_loop<{args[0]},{'BE' if args[2] == 'true' else 'LE'}>"
+    if k == "k_seg":
+        return f"k_seg<{args[0]},rx>" if args[2] == "true" else f"k_seg<{args[0]}>"
+    if k == "k_rag":
+        return f"k_rag<{args[0]},{args[1]}>"
     return k
 
 
@@ -51,7 +55,7 @@ def per_launch(path):
 
 def main(prof_dir, out_path):
     res = {}
-    for c in "234":
+    for c in "2346":
         cfg = f"config{c}"
         fpath = os.path.join(prof_dir, f"pmc_FETCH_SIZE_c{c}", "run_counter_collection.csv")
         wpath = os.path.join(prof_dir, f"pmc_WRITE_SIZE_c{c}", "run_counter_collection.csv")

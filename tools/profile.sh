@@ -9,7 +9,7 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-for cfg in 3 2 4; do
+for cfg in ${CFGS:-3 2 4 6}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c$cfg" -o run -- \
     python3 "$ROOT/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --no-extra --no-e2e \
     > "$OUT/bench_c${cfg}_under_trace.json"
