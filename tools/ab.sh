@@ -1,0 +1,9 @@
+#!/bin/bash
+# Variant / grid A/B on the GPU box (measurement only): tools/ab.sh "<cfg> <VAR=val ...>" ...
+# Each argument is one kbench run: a config number followed by env assignments.
+set -u
+for spec in "$@"; do
+  read -r cfg envs <<< "$spec"
+  echo "== config $cfg ${envs:-default}"
+  env $envs timeout -k 5 120 tools/kbench "$cfg" || exit 1
+done

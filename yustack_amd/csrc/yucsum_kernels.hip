@@ -82,6 +82,7 @@ struct BatchArgs {
   uint32_t len;
   uint32_t initial;
   uint32_t uf;    // k_small: steps u < uf hold only full chunks
+  uint32_t xcd;   // 1: XCD-aware block order (grid_wave)
   int mode;
 };
 
@@ -163,6 +164,24 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v) {
   if (G >= 32) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); // row_bcast:15
   if (G >= 64) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); // row_bcast:31
   return v;
+}
+
+// This wave's index in the grid's packet order. Blocks are dealt round-robin
+// over the 8 XCDs (blocks b and b+8 share an L2), so with xcd set the order is
+// swizzled to give each XCD a contiguous run of logical blocks: the one
+// 128-byte line two neighbouring packets (or 64-packet chunks) share is then
+// fetched by a single L2, at about the same time, instead of by two. Bijective
+// for any grid size (XCDs x < n%8 hold one block more). Speed only: no
+// correctness depends on where a block runs. Off by default (see use_xcd).
+__device__ __forceinline__ uint64_t grid_wave(uint32_t xcd) {
+  const uint32_t b = blockIdx.x, n = gridDim.x;
+  uint32_t lb = b;
+  if (xcd) {
+    const uint32_t x = b & 7u, i = b >> 3, q = n >> 3, r = n & 7u;
+    lb = (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + i;
+  }
+  return (uint64_t)lb * (blockDim.x >> 6) +
+         (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -418,8 +437,7 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t gl = lane & (G - 1);
   const uint32_t gw = lane / G;
-  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
-                        (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave = grid_wave(A.xcd);
   const uint64_t step = (uint64_t)gridDim.x * (blockDim.x >> 6) * GPW;
   const int mode = A.mode;
   const bool ipv4 = mode_is_ipv4(mode);
@@ -517,8 +535,7 @@ __global__ __launch_bounds__(256) void k_tiny(BatchArgs A) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t j = lane & (G - 1);
   const uint32_t g = lane / G;
-  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
-                        (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave = grid_wave(A.xcd);
   const uint64_t step = (uint64_t)gridDim.x * (blockDim.x >> 6) * 64u;
   const SidePtrs sp = side_ptrs(A);
   const uint32_t E = A.len;  // window base = packet start (4-aligned)
@@ -611,8 +628,7 @@ template <int U, int NT, bool BE>
 __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
   constexpr uint32_t W = 64u * 16u * U;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
-                        (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave = grid_wave(A.xcd);
   const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const int mode = A.mode;
   const bool ipv4 = mode_is_ipv4(mode);
@@ -804,8 +820,7 @@ __global__ __launch_bounds__(256) void k_rag(BatchArgs A) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t gl = lane & (G - 1);
   const uint32_t gw = lane / G;
-  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
-                        (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wave = grid_wave(A.xcd);
   const uint64_t step = (uint64_t)gridDim.x * (blockDim.x >> 6) * GPW;
   const int mode = A.mode;
   const bool ipv4 = mode_is_ipv4(mode);
@@ -1070,7 +1085,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   __shared__ uint32_t s_pre[4][NC];  // chunk-exclusive prefixes (L, then T)
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const uint64_t wave = grid_wave(A.xcd);
   const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const int mode = A.mode;
   const bool tx = mode_is_tx(mode);
@@ -1410,6 +1425,15 @@ int use_nt() {
   return v;
 }
 
+// YU_XCD: 1 = XCD-aware block order (grid_wave), 0 (default) = plain blockIdx.
+// Measured (round 1, tools/ab.sh): no gain on any config — these kernels
+// share at most one line between neighbouring blocks, and the Infinity Cache
+// already absorbs its second fetch — and -1..3 % on configs 2/3, so it is off.
+int use_xcd() {
+  static int v = env_int("YU_XCD", 0, 1, 0);
+  return v;
+}
+
 int hip_status(hipError_t e) {
   if (e == hipSuccess) return YU_OK;
   if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return YU_ENODEV;
@@ -1428,7 +1452,9 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu(v.G);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(v.fn[use_nt()], dim3((unsigned)blocks), dim3(256), 0, stream, A);
+  BatchArgs a = A;
+  a.xcd = (uint32_t)use_xcd();
+  hipLaunchKernelGGL(v.fn[use_nt()], dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
 
