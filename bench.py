@@ -226,6 +226,22 @@ def end_to_end(w: Workload, reps: int = 3):
     torch.cuda.synchronize()
     res["matches_device_path"] = bool(np.array_equal(out, w.out.cpu().numpy()))
     res["bytes"] = w.bytes
+    ndev = torch.cuda.device_count()
+    if ndev > 1:  # yu_csum_batch_host_uniform_multi: one shard per visible GPU, each on its own PCIe link
+        devs = list(range(ndev))
+        out2 = np.empty(w.n, np.uint16)
+        try:
+            batch.checksum_host_uniform(pinned, w.L, w.L, w.n, w.mode, initial_arr=init, addrs=addrs,
+                                        out=out2, device=devs)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                batch.checksum_host_uniform(pinned, w.L, w.L, w.n, w.mode, initial_arr=init, addrs=addrs,
+                                            out=out2, device=devs)
+            dt = (time.perf_counter() - t0) / reps
+            res[f"pinned_{ndev}gpu_GiB_s"] = round(w.bytes / dt / GIB, 2)
+            res[f"pinned_{ndev}gpu_matches"] = bool(np.array_equal(out2, out))
+        except Exception as e:  # reported, never fatal to the bench line
+            res[f"pinned_{ndev}gpu_error"] = str(e)[:200]
     return res
 
 

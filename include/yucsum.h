@@ -240,6 +240,34 @@ int yu_csum_batch_host_iov(const yu_iovec *iov, const uint64_t *first_iov,
                            uint16_t initial, const uint8_t *h_addrs,
                            uint16_t *h_out, int device);
 
+/* Multi-GPU host path (SURVEY.md §8b `yu_csum_batch_host(..., ngpu)`, §8e):
+ * the same three calls with the batch split into ndev contiguous shards, one
+ * per entry of `devices` (a device may be listed more than once), each shard
+ * run through the single-device pipeline on that device by a persistent
+ * per-device worker thread, all at once. Packets are independent, so there
+ * is no exchange: shard i writes h_out[first_i, first_i + n_i). Uniform and
+ * iovec batches split by packet count, ragged batches on the packet boundary
+ * nearest an even split of the bytes (balanced PCIe traffic). Synchronous;
+ * returns the first failing shard's status (YU_EINVAL for ndev < 1 or > 64,
+ * YU_ENODEV for a device index out of range). */
+int yu_csum_batch_host_uniform_multi(const uint8_t *h_data, uint64_t stride,
+                                     uint32_t len, uint64_t n, int mode,
+                                     const uint16_t *h_initial_arr,
+                                     uint16_t initial, const uint8_t *h_addrs,
+                                     uint16_t *h_out, const int *devices,
+                                     int ndev);
+int yu_csum_batch_host_ragged_multi(const uint8_t *h_data,
+                                    const uint64_t *h_offsets, uint64_t n,
+                                    int mode, const uint16_t *h_initial_arr,
+                                    uint16_t initial, const uint8_t *h_addrs,
+                                    uint16_t *h_out, const int *devices,
+                                    int ndev);
+int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t *first_iov,
+                                 uint64_t n, int mode,
+                                 const uint16_t *h_initial_arr,
+                                 uint16_t initial, const uint8_t *h_addrs,
+                                 uint16_t *h_out, const int *devices, int ndev);
+
 /* ------------------------------------------------------------------ */
 /* Introspection.                                                      */
 /* ------------------------------------------------------------------ */

@@ -75,6 +75,17 @@ def test_batched_entry_points_fail_without_gpu():
     rc = L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 4, 8, None, 0, None,
                                   ctypes.addressof(out), 0)
     assert rc == _lib.YU_ENODEV
+    devs = (ctypes.c_int * 2)(0, 0)
+    pd = ctypes.addressof(devs)
+    rc = L.yu_csum_batch_host_uniform_multi(ctypes.addressof(buf), 16, 16, 4, 0, None, 0, None,
+                                            ctypes.addressof(out), pd, 2)
+    assert rc == _lib.YU_ENODEV
+    rc = L.yu_csum_batch_host_ragged_multi(ctypes.addressof(buf), ctypes.addressof(offs), 4, 0, None, 0,
+                                           None, ctypes.addressof(out), pd, 2)
+    assert rc == _lib.YU_ENODEV
+    rc = L.yu_csum_batch_host_iov_multi(ctypes.addressof(iov), ctypes.addressof(first), 4, 8, None, 0, None,
+                                        ctypes.addressof(out), pd, 2)
+    assert rc == _lib.YU_ENODEV
 
 
 def test_argument_validation_precedes_device():
@@ -103,6 +114,18 @@ def test_argument_validation_precedes_device():
                                     o, 0) == _lib.YU_EINVAL
     assert L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 1, 9, None, 0, None,
                                     o, 0) == _lib.YU_EINVAL  # mode
+    # multi-GPU host calls: device list and batch checked before any device work
+    devs = (ctypes.c_int * 2)(0, 0)
+    pd = ctypes.addressof(devs)
+    assert L.yu_csum_batch_host_uniform_multi(p, 16, 16, 4, 0, None, 0, None, o, None, 2) == _lib.YU_EINVAL
+    assert L.yu_csum_batch_host_uniform_multi(p, 16, 16, 4, 0, None, 0, None, o, pd, 0) == _lib.YU_EINVAL
+    assert L.yu_csum_batch_host_uniform_multi(p, 16, 16, 4, 0, None, 0, None, o, pd, 65) == _lib.YU_EINVAL
+    assert L.yu_csum_batch_host_uniform_multi(p, 16, 70000, 4, 2, None, 0, None, o, pd, 2) == _lib.YU_EINVAL
+    assert L.yu_csum_batch_host_uniform_multi(p, 16, 16, 0, 0, None, 0, None, o, pd, 2) == 0  # empty
+    assert L.yu_csum_batch_host_ragged_multi(p, ctypes.addressof(bad), 4, 0, None, 0, None, o, pd,
+                                             2) == _lib.YU_EINVAL
+    assert L.yu_csum_batch_host_iov_multi(ctypes.addressof(iov), ctypes.addressof(first), 1, 0, None, 0,
+                                          None, o, pd, 2) == _lib.YU_EINVAL
 
 
 def test_python_front_end_refuses_cpu_tensors():

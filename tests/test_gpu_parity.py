@@ -344,6 +344,43 @@ def test_host_ragged_and_iov_paths(dev, oracle_c):
     assert np.array_equal(got, want)
 
 
+def test_host_multi_device_paths(dev, oracle_c):
+    """Multi-GPU host calls (yu_csum_batch_host_*_multi): one shard per listed
+    device on its own worker thread. On a one-GPU box the list repeats device 0,
+    which exercises the split, the per-worker staging and the result placement."""
+    import rxgen
+    rng = np.random.default_rng(29)
+    ndev = max(1, torch.cuda.device_count())
+    for devs in ([0], [0, 0], [0, 0, 0], list(range(ndev)) * 2):
+        n, L = 50001, 1500
+        host = _rand(rng, n * L)
+        host[12::L] = 0x50
+        addrs = _rand(rng, 8 * n)
+        got = batch.checksum_host_uniform(host, L, L, n, "tcp", addrs=addrs, device=devs)
+        want = oracle_c.batch(host, O.MODE_TCP, stride=L, length=L, n=n, addrs=addrs, threads=8)
+        assert np.array_equal(got, want), devs
+        lens = rng.integers(0, 9001, size=7777)
+        lens[:5] = 0  # empty packets at a shard edge
+        offs = np.zeros(lens.size + 1, np.uint64)
+        offs[1:] = np.cumsum(lens)
+        blob = _rand(rng, int(offs[-1]))
+        init = rng.integers(0, 65536, size=lens.size, dtype=np.uint16)
+        got = batch.checksum_host_ragged(blob, offs, "raw", initial_arr=init, device=devs)
+        want = oracle_c.batch(blob, O.MODE_RAW, offsets=offs, initial_arr=init, threads=8)
+        assert np.array_equal(got, want), devs
+        rblob, roffs = rxgen.rx_batch(rng, 999, lo=0, hi=1480)
+        pkts = [[rblob[int(roffs[i]):int(roffs[i + 1])]] for i in range(roffs.size - 1)]
+        got = batch.checksum_host_iov(pkts, "verify_rx", device=devs)
+        assert np.array_equal(got, oracle_c.batch(rblob, O.MODE_VERIFY_RX, offsets=roffs)), devs
+    # more shards than packets: empty shards are skipped
+    host = _rand(rng, 3 * 64)
+    got = batch.checksum_host_uniform(host, 64, 64, 3, "raw", device=[0] * 5)
+    assert np.array_equal(got, oracle_c.batch(host, O.MODE_RAW, stride=64, length=64, n=3))
+    from yustack_amd._lib import YuError
+    with pytest.raises(YuError):
+        batch.checksum_host_uniform(host, 64, 64, 3, "raw", device=[0, 99])
+
+
 def test_errors_are_loud(dev):
     from yustack_amd._lib import YuError
     d = torch.zeros(1 << 17, dtype=torch.uint8, device=dev)

@@ -18,6 +18,8 @@ EXPORTS = (
     "yu_csum_batch_uniform", "yu_csum_batch_ragged",
     "yu_csum_fill_uniform", "yu_csum_fill_ragged",
     "yu_csum_batch_host_uniform", "yu_csum_batch_host_ragged", "yu_csum_batch_host_iov",
+    "yu_csum_batch_host_uniform_multi", "yu_csum_batch_host_ragged_multi",
+    "yu_csum_batch_host_iov_multi",
     "yu_abi_version", "yu_strerror", "yu_device_count", "yu_uniform_variant",
     "yu_ragged_variant",
 )
@@ -71,6 +73,12 @@ def lib() -> ctypes.CDLL:
     L.yu_csum_batch_host_ragged.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, i32]
     L.yu_csum_batch_host_iov.restype = i32
     L.yu_csum_batch_host_iov.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, i32]
+    L.yu_csum_batch_host_uniform_multi.restype = i32
+    L.yu_csum_batch_host_uniform_multi.argtypes = [vp, u64, u32, u64, i32, vp, u16, vp, vp, vp, i32]
+    L.yu_csum_batch_host_ragged_multi.restype = i32
+    L.yu_csum_batch_host_ragged_multi.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, vp, i32]
+    L.yu_csum_batch_host_iov_multi.restype = i32
+    L.yu_csum_batch_host_iov_multi.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, vp, i32]
     L.yu_abi_version.restype = i32
     L.yu_abi_version.argtypes = []
     L.yu_strerror.restype = c.c_char_p

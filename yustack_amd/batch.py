@@ -148,10 +148,11 @@ def checksum_ragged(data: torch.Tensor, offsets: torch.Tensor, mode="raw", *, in
 def checksum_host_uniform(data: np.ndarray, stride: int, length: int, n: int, mode="raw", *,
                           initial: int = 0, initial_arr: np.ndarray | None = None,
                           addrs: np.ndarray | None = None, out: np.ndarray | None = None,
-                          device: int = 0) -> np.ndarray:
+                          device: int | list[int] = 0) -> np.ndarray:
     """Host-memory batch in, host-memory results out (pinned staging + pipelined
     H2D/kernel/D2H inside the library). ``data`` may be a numpy array or a pinned
-    torch CPU tensor (then the copy engine reads it directly)."""
+    torch CPU tensor (then the copy engine reads it directly). ``device`` may be a
+    list of device indices: one shard per GPU, all at once."""
     m = _mode(mode)
     if isinstance(data, torch.Tensor):
         if data.is_cuda or data.dtype != torch.uint8 or not data.is_contiguous():
@@ -172,11 +173,23 @@ def checksum_host_uniform(data: np.ndarray, stride: int, length: int, n: int, mo
         optr = out.data_ptr()
     else:
         optr = out.ctypes.data
-    rc = lib().yu_csum_batch_host_uniform(dptr, stride, length, n, m,
-                                          None if ia is None else ia.ctypes.data, initial & 0xFFFF,
-                                          None if ad is None else ad.ctypes.data, optr, device)
-    check(rc, "yu_csum_batch_host_uniform")
+    args = (dptr, stride, length, n, m, None if ia is None else ia.ctypes.data, initial & 0xFFFF,
+            None if ad is None else ad.ctypes.data, optr)
+    _host_call("yu_csum_batch_host_uniform", args, device)
     return out
+
+
+def _host_call(name: str, args: tuple, device) -> None:
+    """``device`` an int: the single-GPU host call. A sequence of ints: the
+    ``_multi`` variant, the batch split into one shard per listed device
+    (include/yucsum.h)."""
+    import ctypes
+    if isinstance(device, (list, tuple)):
+        devs = (ctypes.c_int * max(1, len(device)))(*[int(d) for d in device])
+        rc = getattr(lib(), name + "_multi")(*args, devs, len(device))
+        check(rc, name + "_multi")
+    else:
+        check(getattr(lib(), name)(*args, int(device)), name)
 
 
 def _host_side(n, initial_arr, addrs, out):
@@ -192,7 +205,8 @@ def _host_side(n, initial_arr, addrs, out):
 
 
 def checksum_host_ragged(data, offsets, mode="raw", *, initial: int = 0, initial_arr=None,
-                         addrs=None, out: np.ndarray | None = None, device: int = 0) -> np.ndarray:
+                         addrs=None, out: np.ndarray | None = None,
+                         device: int | list[int] = 0) -> np.ndarray:
     """Ragged host batch (packet i = data[offsets[i]:offsets[i+1]], e.g. a tun read
     burst) through the pinned, pipelined host path (yu_csum_batch_host_ragged)."""
     m = _mode(mode)
@@ -210,15 +224,15 @@ def checksum_host_ragged(data, offsets, mode="raw", *, initial: int = 0, initial
     if n and int(offs[-1]) > dlen:
         raise ValueError("offsets run past data")
     ia, ad, out = _host_side(n, initial_arr, addrs, out)
-    rc = lib().yu_csum_batch_host_ragged(dptr, offs.ctypes.data, n, m,
-                                         None if ia is None else ia.ctypes.data, initial & 0xFFFF,
-                                         None if ad is None else ad.ctypes.data, out.ctypes.data, device)
-    check(rc, "yu_csum_batch_host_ragged")
+    args = (dptr, offs.ctypes.data, n, m, None if ia is None else ia.ctypes.data, initial & 0xFFFF,
+            None if ad is None else ad.ctypes.data, out.ctypes.data)
+    _host_call("yu_csum_batch_host_ragged", args, device)
     return out
 
 
 def checksum_host_iov(packets, mode="raw", *, initial: int = 0, initial_arr=None, addrs=None,
-                      out: np.ndarray | None = None, device: int = 0) -> np.ndarray:
+                      out: np.ndarray | None = None,
+                      device: int | list[int] = 0) -> np.ndarray:
     """Scatter-gather host packets: ``packets[i]`` is a list of views (numpy uint8
     arrays / bytes) whose concatenation is packet i, as tundev's readv fills them
     (link/tundev/tundev.go:116-125). Gathered into pinned staging by the library."""
@@ -236,11 +250,10 @@ def checksum_host_iov(packets, mode="raw", *, initial: int = 0, initial_arr=None
         first[i + 1] = len(views)
     iov = (YuIovec * max(1, len(views)))(*[YuIovec(b, l) for b, l in views])
     ia, ad, out = _host_side(n, initial_arr, addrs, out)
-    rc = lib().yu_csum_batch_host_iov(ctypes_addr(iov), first.ctypes.data, n, m,
-                                      None if ia is None else ia.ctypes.data, initial & 0xFFFF,
-                                      None if ad is None else ad.ctypes.data, out.ctypes.data, device)
+    args = (ctypes_addr(iov), first.ctypes.data, n, m, None if ia is None else ia.ctypes.data,
+            initial & 0xFFFF, None if ad is None else ad.ctypes.data, out.ctypes.data)
+    _host_call("yu_csum_batch_host_iov", args, device)
     del keep
-    check(rc, "yu_csum_batch_host_iov")
     return out
 
 

@@ -22,7 +22,14 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "yucsum.h"
 
@@ -326,6 +333,134 @@ int on_device(int device, F &&f) {
 
 bool bad_mode(int mode) { return mode < 0 || mode >= YU_MODE_COUNT; }
 
+// Host offsets are checked here, unlike the device call's: non-decreasing,
+// every packet within the mode's length limit.
+int check_offsets(const uint64_t *off, uint64_t n, int mode) {
+  const uint64_t cap = mode == YU_MODE_RAW ? YU_MAX_RAW_LEN : YU_MAX_TRANSPORT_LEN;
+  for (uint64_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i] || off[i + 1] - off[i] > cap) return YU_EINVAL;
+  return YU_OK;
+}
+
+// Scatter-gather packet index: non-decreasing view ranges, no NULL view with
+// bytes, every packet within the mode's length limit.
+int check_iov(const yu_iovec *iov, const uint64_t *first_iov, uint64_t n, int mode) {
+  const uint64_t cap = mode == YU_MODE_RAW ? YU_MAX_RAW_LEN : YU_MAX_TRANSPORT_LEN;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (first_iov[i + 1] < first_iov[i]) return YU_EINVAL;
+    uint64_t l = 0;
+    for (uint64_t v = first_iov[i]; v < first_iov[i + 1]; ++v) {
+      if (!iov[v].base && iov[v].len) return YU_EINVAL;
+      l += iov[v].len;
+    }
+    if (l > cap) return YU_EINVAL;
+  }
+  return YU_OK;
+}
+
+// Multi-GPU host path: the batch is cut into one contiguous
+// shard per listed device and each shard runs the single-device pipeline on
+// that device's persistent worker thread, so every GPU's PCIe link, copy
+// engines and staging slots work at once. Packets are independent: there is
+// no exchange, each shard writes its own range of h_out. The workers live for
+// the process (their thread-local staging contexts are reused across calls);
+// one worker per device serialises the shards concurrent callers give it.
+class Worker {
+ public:
+  Worker() { std::thread([this] { loop(); }).detach(); }
+  void post(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return !q_.empty(); });
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+};
+
+Worker &worker(int device) {
+  static std::mutex gm;
+  static Worker *w[64];  // process lifetime, never freed (threads are detached)
+  std::lock_guard<std::mutex> l(gm);
+  if (!w[device]) w[device] = new Worker();
+  return *w[device];
+}
+
+bool bad_devices(const int *devices, int ndev) { return !devices || ndev < 1 || ndev > 64; }
+
+int check_devices(const int *devices, int ndev) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return YU_ENODEV;
+  for (int i = 0; i < ndev; ++i)
+    if (devices[i] < 0 || devices[i] >= count || devices[i] >= 64) return YU_ENODEV;
+  return YU_OK;
+}
+
+// Runs shard(i, first, cnt) for the shards [bounds[i], bounds[i+1]) on
+// worker(devices[i]) and waits for all of them; returns the first failure.
+int fan_out(const int *devices, int ndev, const std::vector<uint64_t> &bounds,
+            const std::function<int(int, uint64_t, uint64_t)> &shard) {
+  std::mutex m;
+  std::condition_variable cv;
+  int pending = 0, rc = YU_OK;
+  for (int i = 0; i < ndev; ++i) {
+    const uint64_t a = bounds[i], b = bounds[i + 1];
+    if (a == b) continue;
+    {
+      std::lock_guard<std::mutex> l(m);
+      ++pending;
+    }
+    worker(devices[i]).post([&, i, a, b] {
+      const int r = shard(i, a, b - a);
+      std::lock_guard<std::mutex> l(m);
+      if (r != YU_OK && rc == YU_OK) rc = r;
+      if (--pending == 0) cv.notify_all();
+    });
+  }
+  std::unique_lock<std::mutex> l(m);
+  cv.wait(l, [&] { return pending == 0; });
+  return rc;
+}
+
+// Even packet counts (uniform, iovec).
+std::vector<uint64_t> even_bounds(uint64_t n, int ndev) {
+  std::vector<uint64_t> b(ndev + 1);
+  for (int i = 0; i <= ndev; ++i) b[i] = (uint64_t)((unsigned __int128)n * i / ndev);
+  return b;
+}
+
+// Packet boundaries closest below an even split of the bytes (ragged), as
+// yustack_amd/shard.py does for the device-resident bench.
+std::vector<uint64_t> byte_bounds(const uint64_t *off, uint64_t n, int ndev) {
+  std::vector<uint64_t> b(ndev + 1);
+  const uint64_t o0 = off[0], tot = off[n] - off[0];
+  b[0] = 0;
+  b[ndev] = n;
+  for (int i = 1; i < ndev; ++i) {
+    const uint64_t target = o0 + (uint64_t)((unsigned __int128)tot * i / ndev);
+    uint64_t k = (uint64_t)(std::lower_bound(off, off + n + 1, target) - off);
+    if (k > n) k = n;
+    b[i] = std::max(k, b[i - 1]);
+  }
+  return b;
+}
+
 }  // namespace
 
 extern "C" int yu_csum_batch_host_uniform(const uint8_t *h_data,
@@ -359,10 +494,7 @@ extern "C" int yu_csum_batch_host_ragged(const uint8_t *h_data,
   if (bad_mode(mode) || !h_out) return YU_EINVAL;
   if (n == 0) return YU_OK;
   if (!h_offsets || (!h_data && h_offsets[n] != h_offsets[0])) return YU_EINVAL;
-  const uint64_t cap = mode == YU_MODE_RAW ? YU_MAX_RAW_LEN : YU_MAX_TRANSPORT_LEN;
-  for (uint64_t i = 0; i < n; ++i)  // host offsets: checked here, unlike the device call
-    if (h_offsets[i + 1] < h_offsets[i] || h_offsets[i + 1] - h_offsets[i] > cap)
-      return YU_EINVAL;
+  if (int rc = check_offsets(h_offsets, n, mode)) return rc;
   return on_device(device, [&](Ctx &c) {
     RaggedLayout L{h_data, h_offsets, n, mode, initial, is_pinned(h_data)};
     return pipeline(c, L, n, h_initial_arr, h_addrs, h_out);
@@ -377,18 +509,65 @@ extern "C" int yu_csum_batch_host_iov(const yu_iovec *iov,
   if (bad_mode(mode) || !h_out) return YU_EINVAL;
   if (n == 0) return YU_OK;
   if (!first_iov || (!iov && first_iov[n] != first_iov[0])) return YU_EINVAL;
-  const uint64_t cap = mode == YU_MODE_RAW ? YU_MAX_RAW_LEN : YU_MAX_TRANSPORT_LEN;
-  for (uint64_t i = 0; i < n; ++i) {
-    if (first_iov[i + 1] < first_iov[i]) return YU_EINVAL;
-    uint64_t l = 0;
-    for (uint64_t v = first_iov[i]; v < first_iov[i + 1]; ++v) {
-      if (!iov[v].base && iov[v].len) return YU_EINVAL;
-      l += iov[v].len;
-    }
-    if (l > cap) return YU_EINVAL;
-  }
+  if (int rc = check_iov(iov, first_iov, n, mode)) return rc;
   return on_device(device, [&](Ctx &c) {
     IovLayout L{iov, first_iov, n, mode, initial};
     return pipeline(c, L, n, h_initial_arr, h_addrs, h_out);
+  });
+}
+
+extern "C" int yu_csum_batch_host_uniform_multi(const uint8_t *h_data, uint64_t stride,
+                                                uint32_t len, uint64_t n, int mode,
+                                                const uint16_t *h_initial_arr,
+                                                uint16_t initial, const uint8_t *h_addrs,
+                                                uint16_t *h_out, const int *devices,
+                                                int ndev) {
+  if (bad_mode(mode) || !h_out || bad_devices(devices, ndev)) return YU_EINVAL;
+  if (n == 0) return YU_OK;
+  if (!h_data && len) return YU_EINVAL;
+  if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
+  if (len > YU_MAX_RAW_LEN) return YU_EINVAL;
+  if (int rc = check_devices(devices, ndev)) return rc;
+  return fan_out(devices, ndev, even_bounds(n, ndev), [&](int i, uint64_t a, uint64_t cnt) {
+    return yu_csum_batch_host_uniform(h_data ? h_data + a * stride : nullptr, stride, len, cnt,
+                                      mode, h_initial_arr ? h_initial_arr + a : nullptr, initial,
+                                      h_addrs ? h_addrs + 8 * a : nullptr, h_out + a, devices[i]);
+  });
+}
+
+extern "C" int yu_csum_batch_host_ragged_multi(const uint8_t *h_data,
+                                               const uint64_t *h_offsets, uint64_t n,
+                                               int mode, const uint16_t *h_initial_arr,
+                                               uint16_t initial, const uint8_t *h_addrs,
+                                               uint16_t *h_out, const int *devices,
+                                               int ndev) {
+  if (bad_mode(mode) || !h_out || bad_devices(devices, ndev)) return YU_EINVAL;
+  if (n == 0) return YU_OK;
+  if (!h_offsets || (!h_data && h_offsets[n] != h_offsets[0])) return YU_EINVAL;
+  if (int rc = check_offsets(h_offsets, n, mode)) return rc;
+  if (int rc = check_devices(devices, ndev)) return rc;
+  return fan_out(devices, ndev, byte_bounds(h_offsets, n, ndev),
+                 [&](int i, uint64_t a, uint64_t cnt) {
+                   return yu_csum_batch_host_ragged(
+                       h_data, h_offsets + a, cnt, mode,
+                       h_initial_arr ? h_initial_arr + a : nullptr, initial,
+                       h_addrs ? h_addrs + 8 * a : nullptr, h_out + a, devices[i]);
+                 });
+}
+
+extern "C" int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t *first_iov,
+                                            uint64_t n, int mode,
+                                            const uint16_t *h_initial_arr, uint16_t initial,
+                                            const uint8_t *h_addrs, uint16_t *h_out,
+                                            const int *devices, int ndev) {
+  if (bad_mode(mode) || !h_out || bad_devices(devices, ndev)) return YU_EINVAL;
+  if (n == 0) return YU_OK;
+  if (!first_iov || (!iov && first_iov[n] != first_iov[0])) return YU_EINVAL;
+  if (int rc = check_iov(iov, first_iov, n, mode)) return rc;
+  if (int rc = check_devices(devices, ndev)) return rc;
+  return fan_out(devices, ndev, even_bounds(n, ndev), [&](int i, uint64_t a, uint64_t cnt) {
+    return yu_csum_batch_host_iov(iov, first_iov + a, cnt, mode,
+                                  h_initial_arr ? h_initial_arr + a : nullptr, initial,
+                                  h_addrs ? h_addrs + 8 * a : nullptr, h_out + a, devices[i]);
   });
 }
