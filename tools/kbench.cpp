@@ -64,16 +64,19 @@ int main(int argc, char **argv) {
     uint64_t *d_off = nullptr;
     if (cfg == 2) { L = 64; mode = YU_MODE_RAW; bytes = n * L; alg = bytes + 4 * n; }
     if (cfg == 3) { L = 1500; mode = YU_MODE_TCP; bytes = n * L; alg = bytes + 10 * n; }
-    if (cfg == 4 || cfg == 5 || cfg == 6) {
+    if (cfg >= 4 && cfg <= 8) {
       // 4: BASELINE config 4 (U{64..9000}); 5: tun-like U{64..1500}; 6: U{40..200}
-      const int lo = cfg == 4 ? 64 : (cfg == 5 ? 64 : 40);
-      const int hi = cfg == 4 ? 9000 : (cfg == 5 ? 1500 : 200);
+      // (RAW + initial); 7: U{64..1500} TCP segments, 8: U{40..200} UDP (TX kinds, addrs)
+      const int lo = (cfg == 4 || cfg == 5 || cfg == 7) ? 64 : 40;
+      const int hi = cfg == 4 ? 9000 : ((cfg == 5 || cfg == 7) ? 1500 : 200);
+      if (cfg == 7) mode = YU_MODE_TCP;
+      if (cfg == 8) mode = YU_MODE_UDP;
       std::mt19937_64 rng(4);
       std::uniform_int_distribution<int> d(lo, hi);
       std::vector<uint64_t> off(n + 1, 0);
       for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + d(rng);
       bytes = off[n];
-      alg = bytes + 8 * (n + 1) + 4 * n;
+      alg = bytes + 8 * (n + 1) + (mode == YU_MODE_RAW ? 4 : 10) * n;
       CK(hipMalloc(&d_off, (n + 1) * 8));
       CK(hipMemcpy(d_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
     }
@@ -85,7 +88,9 @@ int main(int argc, char **argv) {
     }
     CK(hipDeviceSynchronize());
     auto launch = [&](int k) {
-      int rc = d_off ? yu_csum_batch_ragged(bufs[k % R], d_off, n, mode, init, 0, nullptr, out, nullptr)
+      const bool tx = mode != YU_MODE_RAW;
+      int rc = d_off ? yu_csum_batch_ragged(bufs[k % R], d_off, n, mode, tx ? nullptr : init, 0,
+                                            tx ? addrs : nullptr, out, nullptr)
                      : yu_csum_batch_uniform(bufs[k % R], L, L, n, mode, cfg == 2 ? init : nullptr, 0,
                                              cfg == 3 ? addrs : nullptr, out, nullptr);
       if (rc) { fprintf(stderr, "rc %d\n", rc); exit(1); }
@@ -101,7 +106,7 @@ int main(int argc, char **argv) {
       double s = ms / 1e3 / reps;
       printf("config%d round %d: %8.1f us/launch  %7.1f GB/s alg  (%.3f of 8 TB/s)  %s\n", cfg, r, s * 1e6,
              alg / s / 1e9, alg / s / 8e12,
-             d_off ? (getenv("YU_RAGGED") ? getenv("YU_RAGGED") : "seg")
+             d_off ? yu_ragged_variant(mode)
                    : yu_uniform_variant(L, L, mode, (uintptr_t)bufs[0] & 15));
     }
     for (auto b : bufs) CK(hipFree(b));

@@ -1077,8 +1077,16 @@ __device__ __forceinline__ void rx_parse(SegRx &rx, uint32_t sh, uint64_t len, u
   if (!valid) hl = tl = 0;
 }
 
-template <int U, int NT, bool RX>
+// Kinds of k_seg by the points a lane evaluates (compile-time, so a kind
+// carries no code or registers for the others): plain (RAW / VERIFY_TCP /
+// VERIFY_UDP: start and end), TX (UDP / TCP / ICMP: + the checksum field's
+// two ends), RX (VERIFY_RX: + header and transport ends).
+constexpr int kSegPlain = 0, kSegTx = 1, kSegRx = 2;
+
+template <int U, int NT, int K>
 __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
+  constexpr bool RX = K == kSegRx;
+  constexpr int NP = K == kSegPlain ? 2 : 4;  // point slots in use
   constexpr uint32_t T = 64u * 16u * U;
   constexpr uint32_t NC = 64u * U;  // chunks per tile
   __shared__ uint4 s_data[4][NC];   // the tile's bytes
@@ -1088,7 +1096,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   const uint64_t wave = grid_wave(A.xcd);
   const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const int mode = A.mode;
-  const bool tx = mode_is_tx(mode);
+  constexpr bool tx = K == kSegTx;
   const uint32_t fld = mode_field(mode);
   const SidePtrs sp = side_ptrs(A);
   const uint64_t data = (uint64_t)(uintptr_t)A.data;
@@ -1129,8 +1137,8 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
       for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pt[i].p = pt[i].t = 0u;
-    exact = mode == YU_MODE_RAW && __any((int)(len > kLEMax));
+    for (int i = 0; i < NP; ++i) pt[i].p = pt[i].t = 0u;
+    exact = K == kSegPlain && mode == YU_MODE_RAW && __any((int)(len > kLEMax));
     carry_l = carry_t = 0u;
   };
   begin_chunk(cur);
@@ -1175,7 +1183,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
     }
     bool here = false;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) here |= pt[i].x - tb < T;
+    for (int i = 0; i < NP; ++i) here |= pt[i].x - tb < T;
     if (RX) {  // a header window [floor4(start), +24) still being gathered
       const uint64_t hs = pt[0].x & ~3ull;
       here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
@@ -1204,7 +1212,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
         }
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NP; ++i) {
         const uint64_t q = pt[i].x - tb;
         if (q < T) {
           const uint32_t k = (uint32_t)q >> 4;
@@ -1217,7 +1225,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
         for (int u = 0; u < U; ++u) s_pre[wid][u * 64 + lane] = ptt[u];
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NP; ++i) {
           const uint64_t q = pt[i].x - tb;
           if (q < T) {
             const uint32_t k = (uint32_t)q >> 4;
@@ -1228,11 +1236,11 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NP; ++i)
       if (pt[i].x - tb == T) pt[i].p = carry_l;
     if (exact) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NP; ++i)
         if (pt[i].x - tb == T) pt[i].t = carry_t;
     }
 
@@ -1272,7 +1280,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
           const uint32_t a = S - b;              // even-address bytes
           v = odd ? a + (b << 8) : (a << 8) + b;
         } else {
-          v = le_to_be(pe - pt[0].p - (pt[3].p - pt[2].p), odd);
+          v = le_to_be(pe - pt[0].p - (tx ? pt[3].p - pt[2].p : 0u), odd);
         }
         const uint64_t len = cur.oy - cur.ox;
         finish_packet(A, p, v, len, cur.sd, A.fill ? A.fill + cur.ox : nullptr,
@@ -1328,10 +1336,21 @@ const Variant kSmall[] = {
 const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, 0, false>, k_loop<4, 1, false>, k_loop<4, 1, false>}, 64, 1};
 const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, 0, true>, k_loop<4, 1, true>, k_loop<4, 1, true>}, 64, 1};
 const Variant kRag = {"k_rag<16,6>", 1536, {k_rag<16, 6, 0>, k_rag<16, 6, 1>, k_rag<16, 6, 2>}, 16, 4};
-const Variant kSeg4 = {"k_seg<4>", 0, {k_seg<4, 0, false>, k_seg<4, 1, false>, k_seg<4, 1, false>}, 64, 64};
-const Variant kSeg8 = {"k_seg<8>", 0, {k_seg<8, 0, false>, k_seg<8, 1, false>, k_seg<8, 1, false>}, 64, 64};
-const Variant kSegRx4 = {"k_seg<4,rx>", 0, {k_seg<4, 0, true>, k_seg<4, 1, true>, k_seg<4, 1, true>}, 64, 64};
-const Variant kSegRx8 = {"k_seg<8,rx>", 0, {k_seg<8, 0, true>, k_seg<8, 1, true>, k_seg<8, 1, true>}, 64, 64};
+#define YU_SEG(U, K, name) \
+  {name, 0, {k_seg<U, 0, K>, k_seg<U, 1, K>, k_seg<U, 1, K>}, 64, 64}
+const Variant kSeg4 = YU_SEG(4, kSegPlain, "k_seg<4>");
+const Variant kSeg8 = YU_SEG(8, kSegPlain, "k_seg<8>");
+const Variant kSegTx4 = YU_SEG(4, kSegTx, "k_seg<4,tx>");
+const Variant kSegTx8 = YU_SEG(8, kSegTx, "k_seg<8,tx>");
+const Variant kSegRx4 = YU_SEG(4, kSegRx, "k_seg<4,rx>");
+const Variant kSegRx8 = YU_SEG(8, kSegRx, "k_seg<8,rx>");
+
+// The k_seg kind for a mode (not the IPv4 header-only modes).
+const Variant &seg_for(bool u8, int mode) {
+  if (mode == YU_MODE_VERIFY_RX) return u8 ? kSegRx8 : kSegRx4;
+  if (mode_is_tx(mode)) return u8 ? kSegTx8 : kSegTx4;
+  return u8 ? kSeg8 : kSeg4;
+}
 
 // Ragged kernel choice: the segmented stream sum with 8 KiB tiles, except for
 // the IPv4 modes, which read only each packet's header (k_rag's per-packet
@@ -1341,10 +1360,10 @@ const Variant kSegRx8 = {"k_seg<8,rx>", 0, {k_seg<8, 0, true>, k_seg<8, 1, true>
 const Variant &pick_ragged(int mode) {
   static const char *f = getenv("YU_RAGGED");
   const bool seg4 = f && strcmp(f, "seg4") == 0;
-  if (f && strcmp(f, "loop") == 0) return mode == YU_MODE_RAW ? kLoopBE : kLoopLE;
-  if (mode == YU_MODE_VERIFY_RX) return seg4 ? kSegRx4 : kSegRx8;
-  if (mode_is_ipv4(mode) || (f && strcmp(f, "rag") == 0)) return kRag;
-  return seg4 ? kSeg4 : kSeg8;
+  const bool rx = mode == YU_MODE_VERIFY_RX;  // only k_seg verifies whole datagrams
+  if (f && strcmp(f, "loop") == 0 && !rx) return mode == YU_MODE_RAW ? kLoopBE : kLoopLE;
+  if (mode_is_ipv4(mode) || (f && strcmp(f, "rag") == 0 && !rx)) return kRag;
+  return seg_for(!seg4, mode);
 }
 
 // Tuning override (measurement only): YU_VARIANT=<name> forces a k_small
@@ -1369,8 +1388,7 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
                                     mode == YU_MODE_VERIFY_UDP);
   if (mode == YU_MODE_VERIFY_RX) return pick_ragged(mode);
   if (const char *f = forced_variant()) {
-    if (strcmp(f, kSeg4.name) == 0) return kSeg4;
-    if (strcmp(f, kSeg8.name) == 0) return kSeg8;
+    if (!mode_is_ipv4(mode) && strncmp(f, "k_seg<", 6) == 0) return seg_for(f[6] == '8', mode);
     for (const Variant &v : kSmall)
       if (strcmp(v.name, f) == 0 && fits(v)) return v;
     for (const Variant &v : kTiny)
