@@ -226,6 +226,20 @@ def end_to_end(w: Workload, reps: int = 3):
     torch.cuda.synchronize()
     res["matches_device_path"] = bool(np.array_equal(out, w.out.cpu().numpy()))
     res["bytes"] = w.bytes
+    # small tun-style bursts through the same host path: per-call latency (fixed
+    # costs of the H2D / kernel / D2H round trip dominate here, not bandwidth)
+    for bn in (64, 1024, 8192):
+        src = pinned[: bn * w.L]
+        o = np.empty(bn, np.uint16)
+        ad = None if addrs is None else addrs[: 8 * bn]
+        ia = None if init is None else init[:bn]
+        for _ in range(10):
+            batch.checksum_host_uniform(src, w.L, w.L, bn, w.mode, initial_arr=ia, addrs=ad, out=o)
+        k = 300
+        t0 = time.perf_counter()
+        for _ in range(k):
+            batch.checksum_host_uniform(src, w.L, w.L, bn, w.mode, initial_arr=ia, addrs=ad, out=o)
+        res[f"burst{bn}_pinned_us_per_call"] = round((time.perf_counter() - t0) / k * 1e6, 1)
     ndev = torch.cuda.device_count()
     if ndev > 1:  # yu_csum_batch_host_uniform_multi: one shard per visible GPU, each on its own PCIe link
         devs = list(range(ndev))

@@ -307,11 +307,26 @@ def test_host_uniform_path(dev, oracle_c):
         got = batch.checksum_host_uniform(host, stride, L, n, mode, addrs=addrs)
         want = oracle_c.batch(host, mode, stride=stride, length=L, n=n, addrs=addrs, threads=8)
         assert np.array_equal(got, want), (n, L, stride)
-    # pinned input goes straight to the copy engine
+    # pinned input goes straight to the copy engine (6 MB: pipelined path) or,
+    # for a small burst, is read by the kernel in place (direct path), also from
+    # an interior, odd address of the pinned allocation, results into pinned memory
     pinned = torch.from_numpy(_rand(rng, 4096 * 1500)).pin_memory()
     got = batch.checksum_host_uniform(pinned, 1500, 1500, 4096, "raw")
     want = oracle_c.batch(pinned.numpy(), O.MODE_RAW, stride=1500, length=1500, n=4096)
     assert np.array_equal(got, want)
+    pout = torch.zeros(64, dtype=torch.int16).pin_memory()
+    for start, n in ((0, 64), (1501, 63), (7, 1)):
+        sub = pinned[start:start + n * 1500]
+        got = batch.checksum_host_uniform(sub, 1500, 1500, n, "raw", out=pout[:n])
+        want = oracle_c.batch(sub.numpy(), O.MODE_RAW, stride=1500, length=1500, n=n)
+        assert np.array_equal(got.numpy().view(np.uint16), want), (start, n)
+    lens = rng.integers(0, 1501, size=300)
+    offs = np.zeros(lens.size + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    offs += 5
+    pr = torch.from_numpy(_rand(rng, int(offs[-1]) + 3)).pin_memory()
+    got = batch.checksum_host_ragged(pr, offs, "raw", initial=0x1234)
+    assert np.array_equal(got, oracle_c.batch(pr.numpy(), O.MODE_RAW, offsets=offs, initial=0x1234))
 
 
 def test_host_ragged_and_iov_paths(dev, oracle_c):
@@ -379,6 +394,58 @@ def test_host_multi_device_paths(dev, oracle_c):
     from yustack_amd._lib import YuError
     with pytest.raises(YuError):
         batch.checksum_host_uniform(host, 64, 64, 3, "raw", device=[0, 99])
+
+
+def test_side_stream_and_graph_replay(dev, oracle_c):
+    """The device entry points run on the caller's stream and, allocating and
+    synchronising nothing, can be captured in a HIP graph (include/yucsum.h):
+    replaying the graph over new bytes in the same buffers gives the new sums."""
+    rng = np.random.default_rng(31)
+    n, L = 4096, 1500
+    lens = rng.integers(40, 1501, size=n)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    addrs = _rand(rng, 8 * n)
+    a_d = _to(dev, addrs)
+    d_u = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    d_r = torch.empty(int(offs[-1]), dtype=torch.uint8, device=dev)
+    o_r = _to(dev, offs.view(np.int64))
+    out_u = torch.empty(n, dtype=torch.uint16, device=dev)
+    out_r = torch.empty(n, dtype=torch.uint16, device=dev)
+
+    def fresh():
+        hu = _rand(rng, n * L)
+        hu[12::L] = 0x50
+        hr = _rand(rng, int(offs[-1]))
+        d_u.copy_(torch.from_numpy(hu))
+        d_r.copy_(torch.from_numpy(hr))
+        return (oracle_c.batch(hu, O.MODE_TCP, stride=L, length=L, n=n, addrs=addrs),
+                oracle_c.batch(hr, O.MODE_UDP, offsets=offs, addrs=addrs))
+
+    def launch():
+        batch.checksum_uniform(d_u, L, L, n, "tcp", addrs=a_d, out=out_u)
+        batch.checksum_ragged(d_r, o_r, "udp", addrs=a_d, out=out_r, validate=False)
+
+    want_u, want_r = fresh()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        launch()
+    s.synchronize()
+    assert np.array_equal(out_u.cpu().numpy(), want_u)
+    assert np.array_equal(out_r.cpu().numpy(), want_r)
+
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        launch()
+    for _ in range(2):
+        want_u, want_r = fresh()
+        out_u.zero_()
+        out_r.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(out_u.cpu().numpy(), want_u)
+        assert np.array_equal(out_r.cpu().numpy(), want_r)
 
 
 def test_errors_are_loud(dev):
