@@ -68,12 +68,14 @@ class Workload:
             nbytes = n * self.L
             self.side = 8 * n  # addrs
             self.name = "config3: 1M x 1500-B TCP segments incl. pseudo-header (sendTCP field value)"
-        elif cfg in (4, 6):
+        elif cfg in (4, 6, 7):
             # 4: ragged 64..9000 B back-to-back, RAW with initial (BASELINE config 4)
             # 6: tun RX burst, 1M whole IPv4 datagrams U{40..1500} B, VERIFY_RX (§8f row 1)
+            # 7: the same with small datagrams U{40..200} B (ACKs, DNS, VoIP)
             self.mode = batch.RAW if cfg == 4 else batch.VERIFY_RX
             rng = np.random.default_rng(cfg)
-            lens = rng.integers(64, 9001, size=n) if cfg == 4 else rng.integers(40, 1501, size=n)
+            hi = {4: 9001, 6: 1501, 7: 201}[cfg]
+            lens = rng.integers(64 if cfg == 4 else 40, hi, size=n)
             offs = np.zeros(n + 1, dtype=np.int64)
             offs[1:] = np.cumsum(lens)
             nbytes = int(offs[-1])
@@ -82,7 +84,7 @@ class Workload:
             self.lens = torch.from_numpy(lens).to(dev)
             self.side = 8 * (n + 1) + (2 * n if cfg == 4 else 0)
             self.name = ("config4: ragged 1M packets U{64..9000} B back-to-back (odd offsets)" if cfg == 4 else
-                         "tun RX: 1M received IPv4 datagrams U{40..1500} B back-to-back, header + TCP "
+                         f"tun RX: 1M received IPv4 datagrams U{{40..{hi - 1}}} B back-to-back, header + TCP "
                          "checksum verification (VERIFY_RX)")
         else:
             raise SystemExit(f"unknown config {cfg}")
@@ -95,7 +97,7 @@ class Workload:
                 v = d.view(n, self.L)
                 v[:, 12] = 0x50
                 v[:, 16:18] = 0
-            if cfg == 6:  # IPv4 header: IHL 5, TotalLength = packet length, protocol TCP
+            if cfg in (6, 7):  # IPv4 header: IHL 5, TotalLength = packet length, protocol TCP
                 s0 = self.offsets[:-1]
                 d[s0] = 0x45
                 d[s0 + 2] = (self.lens >> 8).to(torch.uint8)
@@ -272,7 +274,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 6])
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 6, 7])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip configs 2/4 side measurements")
     ap.add_argument("--cpu-budget", type=float, default=6.0, help="wall seconds for the CPU baseline")
@@ -352,7 +354,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_extra:
         extra = {}
-        for c in (2, 3, 4, 6):
+        for c in (2, 3, 4, 6, 7):
             if c == args.config:
                 continue
             wc = Workload(c, dev, seed=77 + c)

@@ -64,11 +64,12 @@ int main(int argc, char **argv) {
     uint64_t *d_off = nullptr;
     if (cfg == 2) { L = 64; mode = YU_MODE_RAW; bytes = n * L; alg = bytes + 4 * n; }
     if (cfg == 3) { L = 1500; mode = YU_MODE_TCP; bytes = n * L; alg = bytes + 10 * n; }
-    if (cfg >= 4 && cfg <= 8) {
+    if (cfg >= 4 && cfg <= 10) {
       // 4: BASELINE config 4 (U{64..9000}); 5: tun-like U{64..1500}; 6: U{40..200}
       // (RAW + initial); 7: U{64..1500} TCP segments, 8: U{40..200} UDP (TX kinds, addrs)
+      // 9: U{40..600}, 10: U{40..1000} (RAW + initial): small-grid crossover
       const int lo = (cfg == 4 || cfg == 5 || cfg == 7) ? 64 : 40;
-      const int hi = cfg == 4 ? 9000 : ((cfg == 5 || cfg == 7) ? 1500 : 200);
+      const int hi = cfg == 4 ? 9000 : ((cfg == 5 || cfg == 7) ? 1500 : (cfg == 9 ? 600 : (cfg == 10 ? 1000 : 200)));
       if (cfg == 7) mode = YU_MODE_TCP;
       if (cfg == 8) mode = YU_MODE_UDP;
       std::mt19937_64 rng(4);

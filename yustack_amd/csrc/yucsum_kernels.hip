@@ -83,6 +83,7 @@ struct BatchArgs {
   uint32_t initial;
   uint32_t uf;    // k_small: steps u < uf hold only full chunks
   uint32_t xcd;   // 1: XCD-aware block order (grid_wave)
+  uint32_t small_waves;  // k_seg: waves that work on small-packet batches (seg_waves)
   int mode;
 };
 
@@ -1077,6 +1078,29 @@ __device__ __forceinline__ void rx_parse(SegRx &rx, uint32_t sh, uint64_t len, u
   if (!valid) hl = tl = 0;
 }
 
+// Waves that take part in a k_seg launch. The grid is sized for large
+// packets (many tiles per 64-packet chunk). When a ragged batch's packets
+// average under kSegSmallMean bytes, a chunk is one or two tiles, and a wave
+// that handles a single chunk spends its life waiting on two dependent loads
+// (offsets, then bytes). So only A.small_waves waves (3 blocks per CU) work,
+// each streaming several chunks with the next chunk's loads in flight; the
+// other waves exit at once. The mean comes from two scalar loads of the
+// offsets, which the host cannot read without a device synchronisation.
+// Measured (kbench, round 1): U{40..200} 33 -> 25.5 us, U{40..600} 61 -> 58 us,
+// but U{40..1000} 91 -> 93 us and U{64..1500} 127 -> 131 us, so the cut is a
+// 400-byte mean.
+constexpr uint64_t kSegSmallMean = 400;
+
+typedef const __attribute__((address_space(4))) uint64_t c_u64;
+
+__device__ __forceinline__ uint64_t seg_waves(const BatchArgs &A) {
+  const uint64_t all = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  if (!A.offsets || A.small_waves == 0 || A.small_waves >= all) return all;
+  c_u64 *o = (c_u64 *)A.offsets;  // read-only here: scalar loads
+  const uint64_t bytes = o[A.n] - o[0];
+  return bytes < kSegSmallMean * A.n ? (uint64_t)A.small_waves : all;
+}
+
 // Kinds of k_seg by the points a lane evaluates (compile-time, so a kind
 // carries no code or registers for the others): plain (RAW / VERIFY_TCP /
 // VERIFY_UDP: start and end), TX (UDP / TCP / ICMP: + the checksum field's
@@ -1094,7 +1118,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t wave = grid_wave(A.xcd);
-  const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t nwave = seg_waves(A);
   const int mode = A.mode;
   constexpr bool tx = K == kSegTx;
   const uint32_t fld = mode_field(mode);
@@ -1106,7 +1130,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   constexpr uint64_t kNoPt = ~0ull;          // a point slot not in use
 
   uint64_t ch = wave;
-  if (ch * 64u >= A.n) return;
+  if (wave >= nwave || ch * 64u >= A.n) return;
   SegChunk cur, nxt;
   seg_load(A, sp, ch * 64u, lane, cur);
   seg_load(A, sp, (ch + nwave) * 64u, lane, nxt);
@@ -1447,6 +1471,13 @@ int use_nt() {
 // Measured (round 1, tools/ab.sh): no gain on any config — these kernels
 // share at most one line between neighbouring blocks, and the Infinity Cache
 // already absorbs its second fetch — and -1..3 % on configs 2/3, so it is off.
+// YU_SEG_SMALL_BLOCKS: blocks per CU that work on a small-packet ragged
+// batch (seg_waves); 0 = the whole grid.
+int seg_small_blocks() {
+  static int v = env_int("YU_SEG_SMALL_BLOCKS", 0, 64, 3);
+  return v;
+}
+
 int use_xcd() {
   static int v = env_int("YU_XCD", 0, 1, 0);
   return v;
@@ -1472,6 +1503,7 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   if (blocks < 1) blocks = 1;
   BatchArgs a = A;
   a.xcd = (uint32_t)use_xcd();
+  a.small_waves = (uint32_t)cu_count(dev) * 4u * (uint32_t)seg_small_blocks();
   hipLaunchKernelGGL(v.fn[use_nt()], dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
