@@ -5,10 +5,11 @@
 // header/tcp.go, header/udp.go, types/route.go, transport/udp/endpoint.go,
 // transport/tcp/connect.go, network/ipv4/icmp.go and checker/checker.go build
 // unchanged. They bind the scalar entry points of the C ABI (include/yucsum.h,
-// libyucsum.so). Batches go to the GPU through BatchHostUniform.
+// libyucsum.so). Batches go to the GPU through BatchHostUniform, BatchHostRagged
+// and BatchHostPackets (a tun read burst as [][]byte, no copy on the Go side).
 //
 // Status: written against the C ABI; not compiled in the build container (it
-// has no Go toolchain). See INTEGRATION.md for how to build and swap it in.
+// has no Go toolchain). Needs Go >= 1.21 (runtime.Pinner, unsafe.Slice). See INTEGRATION.md for how to build and swap it in.
 package checksum
 
 /*
@@ -22,6 +23,7 @@ import "C"
 import (
 	"errors"
 	"fmt"
+	"runtime"
 	"unsafe"
 )
 
@@ -126,4 +128,99 @@ func BatchHostUniform(data []byte, stride uint64, length uint32, n uint64, mode 
 	default:
 		return fmt.Errorf("checksum: %s (%d)", C.GoString(C.yu_strerror(rc)), int(rc))
 	}
+}
+
+func status(rc C.int) error {
+	switch {
+	case rc == C.YU_OK:
+		return nil
+	case rc == C.YU_ENODEV:
+		return ErrNoDevice
+	default:
+		return fmt.Errorf("checksum: %s (%d)", C.GoString(C.yu_strerror(rc)), int(rc))
+	}
+}
+
+// sideArgs returns the optional per-packet side arrays as C pointers.
+func sideArgs(initial []uint16, addrs []byte) (*C.uint16_t, *C.uint8_t) {
+	var pi *C.uint16_t
+	if len(initial) > 0 {
+		pi = (*C.uint16_t)(unsafe.Pointer(&initial[0]))
+	}
+	var pa *C.uint8_t
+	if len(addrs) > 0 {
+		pa = (*C.uint8_t)(unsafe.Pointer(&addrs[0]))
+	}
+	return pi, pa
+}
+
+// deviceList turns the optional device list into the C (pointer, count) pair
+// of the *_multi calls; a []C.int holds no Go pointers, so it may be passed.
+func deviceList(devices []int) ([]C.int, int) {
+	if len(devices) == 0 {
+		devices = []int{0}
+	}
+	d := make([]C.int, len(devices))
+	for i, v := range devices {
+		d[i] = C.int(v)
+	}
+	return d, len(d)
+}
+
+// BatchHostRagged computes one result per packet of a burst packed back to
+// back in host memory: packet i = data[offsets[i]:offsets[i+1]] (len(offsets)
+// = n+1). initial (n) and addrs (8n) are optional. With several devices the
+// burst is split into one shard per GPU (yu_csum_batch_host_ragged_multi).
+func BatchHostRagged(data []byte, offsets []uint64, mode Mode, initial []uint16, addrs []byte,
+	out []uint16, devices ...int) error {
+	if len(offsets) < 2 {
+		return nil
+	}
+	n := uint64(len(offsets) - 1)
+	if uint64(len(out)) < n || offsets[n] > uint64(len(data)) {
+		return fmt.Errorf("checksum: batch buffers too small")
+	}
+	var pd *C.uint8_t
+	if len(data) > 0 {
+		pd = (*C.uint8_t)(unsafe.Pointer(&data[0]))
+	}
+	pi, pa := sideArgs(initial, addrs)
+	d, nd := deviceList(devices)
+	return status(C.yu_csum_batch_host_ragged_multi(pd, (*C.uint64_t)(unsafe.Pointer(&offsets[0])),
+		C.uint64_t(n), C.int(mode), pi, 0, pa, (*C.uint16_t)(unsafe.Pointer(&out[0])), &d[0], C.int(nd)))
+}
+
+// BatchHostPackets computes one result per packet of a burst given as one
+// slice per packet (buffer.View, buffer/view.go:4), gathered by the library
+// into its pinned staging. The views' Go memory is pinned (runtime.Pinner)
+// for the call, because the C-allocated iovec array holds pointers into it;
+// the library keeps none of them after returning.
+func BatchHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, out []uint16,
+	devices ...int) error {
+	n := len(pkts)
+	if n == 0 {
+		return nil
+	}
+	if len(out) < n {
+		return fmt.Errorf("checksum: batch buffers too small")
+	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	iov := unsafe.Slice((*C.yu_iovec)(C.malloc(C.size_t(n)*C.size_t(unsafe.Sizeof(C.yu_iovec{})))), n)
+	defer C.free(unsafe.Pointer(&iov[0]))
+	first := make([]uint64, n+1)
+	for i, p := range pkts {
+		if len(p) > 0 {
+			pin.Pin(&p[0])
+			iov[i].base = unsafe.Pointer(&p[0])
+		} else {
+			iov[i].base = nil
+		}
+		iov[i].len = C.uint64_t(len(p))
+		first[i+1] = uint64(i + 1)
+	}
+	pi, pa := sideArgs(initial, addrs)
+	d, nd := deviceList(devices)
+	return status(C.yu_csum_batch_host_iov_multi(&iov[0], (*C.uint64_t)(unsafe.Pointer(&first[0])),
+		C.uint64_t(n), C.int(mode), pi, 0, pa, (*C.uint16_t)(unsafe.Pointer(&out[0])), &d[0], C.int(nd)))
 }

@@ -52,3 +52,41 @@ func BenchmarkChecksum1500(b *testing.B) {
 		Checksum(buf, 0)
 	}
 }
+
+// TestBatchHostPackets checks the GPU burst path against the scalar package
+// (skipped without a HIP device).
+func TestBatchHostPackets(t *testing.T) {
+	pkts := make([][]byte, 1000)
+	for i := range pkts {
+		pkts[i] = make([]byte, 40+(i*37)%1461)
+		for j := range pkts[i] {
+			pkts[i][j] = byte(i*131 + j*7)
+		}
+	}
+	out := make([]uint16, len(pkts))
+	if err := BatchHostPackets(pkts, ModeRaw, nil, nil, out); err == ErrNoDevice {
+		t.Skip("no HIP device")
+	} else if err != nil {
+		t.Fatal(err)
+	}
+	for i, p := range pkts {
+		if want := Checksum(p, 0); out[i] != want {
+			t.Fatalf("packet %d: got %#x want %#x", i, out[i], want)
+		}
+	}
+	var blob []byte
+	offs := []uint64{0}
+	for _, p := range pkts {
+		blob = append(blob, p...)
+		offs = append(offs, uint64(len(blob)))
+	}
+	out2 := make([]uint16, len(pkts))
+	if err := BatchHostRagged(blob, offs, ModeRaw, nil, nil, out2, 0, 0); err != nil {
+		t.Fatal(err)
+	}
+	for i := range out {
+		if out2[i] != out[i] {
+			t.Fatalf("ragged packet %d: got %#x want %#x", i, out2[i], out[i])
+		}
+	}
+}

@@ -242,12 +242,59 @@ inline void FillUniform(uint8_t *data, uint64_t stride, uint32_t len, uint64_t n
   if (rc) throw Error(rc, "yu_csum_fill_uniform");
 }
 
-// Host buffers in, host results out (pinned staging + pipelined copies).
+inline void FillRagged(uint8_t *data, const uint64_t *offsets, uint64_t n, Mode m,
+                       uint16_t *out = nullptr, const Side &s = {}, void *stream = nullptr) {
+  int rc = yu_csum_fill_ragged(data, offsets, n, m, s.initial_arr, s.initial, s.addrs, out,
+                               stream);
+  if (rc) throw Error(rc, "yu_csum_fill_ragged");
+}
+
+// Host buffers in, host results out (pinned staging + pipelined copies, or
+// the direct path for bursts up to 4 MiB). Here `Side` holds HOST pointers.
+// A device list shards the batch over several GPUs (the *_multi calls).
 inline void HostUniform(const uint8_t *data, uint64_t stride, uint32_t len, uint64_t n, Mode m,
                         uint16_t *out, const Side &s = {}, int device = 0) {
   int rc = yu_csum_batch_host_uniform(data, stride, len, n, m, s.initial_arr, s.initial,
                                       s.addrs, out, device);
   if (rc) throw Error(rc, "yu_csum_batch_host_uniform");
+}
+
+inline void HostUniform(const uint8_t *data, uint64_t stride, uint32_t len, uint64_t n, Mode m,
+                        uint16_t *out, const Side &s, const std::vector<int> &devices) {
+  int rc = yu_csum_batch_host_uniform_multi(data, stride, len, n, m, s.initial_arr, s.initial,
+                                            s.addrs, out, devices.data(), (int)devices.size());
+  if (rc) throw Error(rc, "yu_csum_batch_host_uniform_multi");
+}
+
+// A tun read burst packed back to back: packet i = data[offsets[i], offsets[i+1]).
+inline void HostRagged(const uint8_t *data, const uint64_t *offsets, uint64_t n, Mode m,
+                       uint16_t *out, const Side &s = {}, int device = 0) {
+  int rc = yu_csum_batch_host_ragged(data, offsets, n, m, s.initial_arr, s.initial, s.addrs,
+                                     out, device);
+  if (rc) throw Error(rc, "yu_csum_batch_host_ragged");
+}
+
+inline void HostRagged(const uint8_t *data, const uint64_t *offsets, uint64_t n, Mode m,
+                       uint16_t *out, const Side &s, const std::vector<int> &devices) {
+  int rc = yu_csum_batch_host_ragged_multi(data, offsets, n, m, s.initial_arr, s.initial,
+                                           s.addrs, out, devices.data(), (int)devices.size());
+  if (rc) throw Error(rc, "yu_csum_batch_host_ragged_multi");
+}
+
+// Scatter-gather packets (the tun endpoint's readv views,
+// link/tundev/tundev.go:116-125): packet i = iov[first_iov[i] .. first_iov[i+1]).
+inline void HostPackets(const yu_iovec *iov, const uint64_t *first_iov, uint64_t n, Mode m,
+                        uint16_t *out, const Side &s = {}, int device = 0) {
+  int rc = yu_csum_batch_host_iov(iov, first_iov, n, m, s.initial_arr, s.initial, s.addrs, out,
+                                  device);
+  if (rc) throw Error(rc, "yu_csum_batch_host_iov");
+}
+
+inline void HostPackets(const yu_iovec *iov, const uint64_t *first_iov, uint64_t n, Mode m,
+                        uint16_t *out, const Side &s, const std::vector<int> &devices) {
+  int rc = yu_csum_batch_host_iov_multi(iov, first_iov, n, m, s.initial_arr, s.initial,
+                                        s.addrs, out, devices.data(), (int)devices.size());
+  if (rc) throw Error(rc, "yu_csum_batch_host_iov_multi");
 }
 
 }  // namespace batch

@@ -14,6 +14,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <random>
 #include <string>
 #include <vector>
@@ -201,6 +202,37 @@ static void test_gpu_batches() {
   batch::Ragged(d_segs, d_soff, n, batch::TCP, d_out, side);  // TX: field taken as 0
   HIPCK(hipMemcpy(out.data(), d_out, n * 2, hipMemcpyDeviceToHost));
   for (uint64_t i = 0; i < n; ++i) EXPECT(out[i] == fields[i], "tcp field %lu", i);
+
+  // the same packets from host memory: back to back, as 4-view scatter-gather
+  // packets (tundev's readv, cuts at 128/384/896), and sharded over a device list
+  batch::Side hside;
+  hside.addrs = addrs.data();
+  std::vector<uint16_t> hout(n, 0xAAAA);
+  batch::HostRagged(segs.data(), soff.data(), n, batch::TCP, hout.data(), hside);
+  for (uint64_t i = 0; i < n; ++i) EXPECT(hout[i] == fields[i], "host tcp field %lu", i);
+  std::vector<yu_iovec> iov;
+  std::vector<uint64_t> first{0};
+  const size_t cuts[] = {128, 128 + 384, 128 + 384 + 896};
+  for (uint64_t i = 0; i < n; ++i) {
+    size_t a = 0;
+    const uint8_t *pk = blob.data() + off[i];
+    const size_t len = off[i + 1] - off[i];
+    for (size_t c : cuts) {
+      if (c >= len) break;
+      iov.push_back({pk + a, c - a});
+      a = c;
+    }
+    iov.push_back({pk + a, len - a});
+    first.push_back(iov.size());
+  }
+  std::fill(hout.begin(), hout.end(), 0xAAAA);
+  batch::HostPackets(iov.data(), first.data(), n, batch::VERIFY_IPV4, hout.data(), {}, {0, 0});
+  for (uint64_t i = 0; i < n; ++i)
+    EXPECT(hout[i] == 0 || hout[i] == 0xffff, "host iov verify_ipv4 %lu", i);
+  std::fill(hout.begin(), hout.end(), 0xAAAA);
+  batch::HostUniform(segs.data(), 1, 20, n, batch::RAW, hout.data(), {}, {0, 0, 0});
+  for (uint64_t i = 0; i < n; ++i)
+    EXPECT(hout[i] == checksum::Checksum(segs.data() + i, 20, 0), "host multi raw %lu", i);
 
   bool threw = false;
   try {
