@@ -11,16 +11,18 @@
  * compiled with -O2 -fno-tree-vectorize this is the "reference-faithful"
  * scalar baseline.
  *
- * Pinning: the reference is Go and no Go toolchain exists in this image, so
- * the reference cannot be executed here; it ships no known-answer vectors
- * (SURVEY.md §8c). This oracle is pinned by (1) RFC 1071 §3's published
- * example, (2) the reference's own test-side verification property
- * (checker/checker.go:32-35,80-92: a correctly filled packet sums to 0 or
- * 0xFFFF), applied to packets built exactly as the reference's test
- * harnesses build them (transport/tcp/testing/context/context.go:164-209,
- * transport/udp/udp_test.go:105-144), and (3) an independent Python twin
- * (oracle/oracle.py) plus a closed-form restatement, cross-checked in
- * tests/test_oracle.c-backed tests and the committed fixtures.
+ * Pinning: the reference is Go and no Go toolchain exists in this image, and
+ * it ships no known-answer vectors. This oracle is pinned by
+ * (1) known answers produced by EXECUTING the reference's own source
+ * (checksum/checksum.go, header/{ipv4,tcp,udp}.go) with a minimal Go-subset
+ * interpreter, tests/golden/goexec.py -> tests/golden/refexec.json (every
+ * batch mode, the Checksum/Combine/PseudoHeaderChecksum functions, the uint32
+ * wrap); (2) RFC 1071 §3's published example; (3) the reference's own
+ * test-side verification property (checker/checker.go:32-35,80-92) on packets
+ * built as its test harnesses build them (transport/tcp/testing/context/
+ * context.go:164-209, transport/udp/udp_test.go:105-144); and (4) an
+ * independent Python twin (oracle/oracle.py) plus a closed form, all checked
+ * in tests/test_oracle.py.
  */
 #include <pthread.h>
 #include <stdint.h>

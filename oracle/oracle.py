@@ -11,12 +11,13 @@ Two independent CPU restatements of yustack's checksum path
 Only ``tests/``, ``__graft_entry__.smoke()`` and bench.py's cpu_baseline leg may
 import this module. The product package ``yustack_amd`` never does.
 
-Pinning status: the reference is Go and cannot be run in
-this image, and it ships no known-answer vectors. This oracle is pinned by RFC 1071
-§3's published example, by the reference's own test-side property
-(checker/checker.go:32-35,80-92) on packets built the way the reference's test
-harnesses build them, and by agreement of the two independent restatements plus the
-closed form below.
+Pinning status: the reference is Go (no toolchain in this image)
+and ships no known-answer vectors. This oracle is pinned by known answers produced by
+executing the reference's own source (checksum/checksum.go, header/{ipv4,tcp,udp}.go)
+with the Go-subset interpreter tests/golden/goexec.py (tests/golden/refexec.json), by
+RFC 1071 §3's published example, by the reference's own test-side property
+(checker/checker.go:32-35,80-92) on packets built the way its test harnesses build
+them, and by agreement of the two independent restatements plus the closed form.
 """
 from __future__ import annotations
 

@@ -501,3 +501,33 @@ def test_full_config4_ragged(dev, oracle_c):
     got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), "raw", initial_arr=_to(dev, init)).cpu().numpy()
     want = oracle_c.batch(d.cpu().numpy(), O.MODE_RAW, offsets=offs, initial_arr=init, threads=16)
     assert np.array_equal(got, want)
+
+
+# ------------------------------------------------------------------ reference-executed vectors
+def test_refexec_vectors_on_gpu(dev):
+    """The HIP path against known answers produced by executing the reference's own Go
+    source (tests/golden/make_refexec.py, tests/golden/goexec.py): every batch mode as
+    a ragged batch (odd offsets included) and the Checksum vectors as RAW packets."""
+    import json
+    import os
+    from test_oracle import REFEXEC, _vec_bytes, refexec_mode_batch
+    ref = json.load(open(REFEXEC))
+    for mode, vecs in ref["modes"].items():
+        m = int(mode)
+        data, offs, addrs, init, want = refexec_mode_batch(vecs, m)
+        got = batch.checksum_ragged(_to(dev, data), _to(dev, offs.view(np.int64)), m,
+                                    addrs=None if addrs is None else _to(dev, addrs),
+                                    initial_arr=None if init is None else _to(dev, init)).cpu().numpy()
+        assert np.array_equal(got, want), (mode, np.nonzero(got != want)[0][:10])
+    pk = [_vec_bytes(v) for v in ref["checksum"]]
+    offs = np.zeros(len(pk) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in pk])
+    data = np.frombuffer(b"".join(pk) + b"\0", np.uint8).copy()
+    init = np.array([v["initial"] for v in ref["checksum"]], np.uint16)
+    got = batch.checksum_ragged(_to(dev, data), _to(dev, offs.view(np.int64)), "raw",
+                                initial_arr=_to(dev, init)).cpu().numpy()
+    assert np.array_equal(got, np.array([v["want"] for v in ref["checksum"]], np.uint16))
+    for v in ref["wrap"]:
+        d = np.full(v["len"], v["fill"], np.uint8)
+        got = batch.checksum_uniform(_to(dev, d), v["len"], v["len"], 1, "raw", initial=v["initial"])
+        assert int(got.cpu().numpy()[0]) == v["want"], v

@@ -175,3 +175,75 @@ def test_oracle_multithreaded_matches_single(oracle_c):
     a = oracle_c.batch(blob, O.MODE_RAW, stride=1500, length=1500, n=1000, threads=1)
     b = oracle_c.batch(blob, O.MODE_RAW, stride=1500, length=1500, n=1000, threads=7)
     assert (a == b).all()
+
+
+# ------------------------------------------------------------------------------
+# Known answers from the reference's own Go source, executed by the Go-subset
+# interpreter tests/golden/goexec.py (tests/golden/make_refexec.py).
+REFEXEC = os.path.join(os.path.dirname(__file__), "golden", "refexec.json")
+
+
+@pytest.fixture(scope="module")
+def refexec():
+    with open(REFEXEC) as f:
+        return json.load(f)
+
+
+def _vec_bytes(v):
+    if "hex" in v:
+        return bytes.fromhex(v["hex"])
+    return bytes(v["len"]) if v["kind"] == "zero" else b"\xff" * v["len"]
+
+
+def test_refexec_checksum_combine_pseudo(refexec, oracle_c):
+    for v in refexec["checksum"]:
+        d = _vec_bytes(v)
+        assert O.checksum(d, v["initial"]) == oracle_c.checksum(d, v["initial"]) == v["want"], v
+    for v in refexec["wrap"]:
+        d = bytes([v["fill"]]) * v["len"]
+        assert oracle_c.checksum(d, v["initial"]) == v["want"]
+    for a, b, want in refexec["combine"]:
+        assert O.checksum_combine(a, b) == oracle_c.combine(a, b) == want
+    for v in refexec["pseudo"]:
+        src, dst = bytes.fromhex(v["src"]), bytes.fromhex(v["dst"])
+        assert O.pseudo_header_checksum(v["proto"], src, dst) == \
+            oracle_c.pseudo_header_checksum(v["proto"], src, dst) == v["want"]
+
+
+def refexec_mode_batch(vecs, mode):
+    """(data, offsets, addrs, initial_arr, want) of one mode's vectors as a ragged batch."""
+    pk = [bytes.fromhex(v["hex"]) for v in vecs]
+    offs = np.zeros(len(pk) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in pk])
+    data = np.frombuffer(b"".join(pk) + b"\0", np.uint8).copy()
+    side = [bytes.fromhex(v["addrs"]) for v in vecs]
+    addrs = np.frombuffer(b"".join(side), np.uint8).copy() if mode in (1, 2, 6, 7) else None
+    init = np.array([int.from_bytes(s[:2], "little") for s in side], np.uint16) if mode == 0 else None
+    return data, offs, addrs, init, np.array([v["want"] for v in vecs], np.uint16)
+
+
+def test_refexec_batch_modes(refexec, oracle_c):
+    assert set(refexec["modes"]) == {str(m) for m in range(9)}
+    for mode, vecs in refexec["modes"].items():
+        m = int(mode)
+        data, offs, addrs, init, want = refexec_mode_batch(vecs, m)
+        got = oracle_c.batch(data, m, offsets=offs, addrs=addrs, initial_arr=init)
+        assert np.array_equal(got, want), mode
+        py = O.batch_ragged_py(data, offs, m, initial_arr=init, addrs=addrs)
+        assert np.array_equal(py, want), mode
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/checksum"), reason="reference tree absent")
+def test_refexec_provenance(refexec):
+    """Re-execute a sample of the fixture from the reference source (where it exists)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import goexec as G
+    it = G.load_reference()
+    for v in refexec["checksum"][::17]:
+        got = it.call("checksum", "Checksum", G.from_bytes(_vec_bytes(v)), G.Int(v["initial"], "uint16"))
+        assert got.v == v["want"]
+    for v in refexec["modes"]["3"][:10]:  # IPv4 header field: ^CalculateChecksum() with the field 0
+        b = bytearray.fromhex(v["hex"])
+        b[10:12] = b"\0\0"
+        assert ~it.method("header", G.from_bytes(bytes(b), "IPv4"), "CalculateChecksum").v & 0xFFFF == v["want"]
