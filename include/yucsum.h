@@ -26,10 +26,13 @@
  *     return a status code. There is no CPU fallback: without a usable GPU
  *     they return a negative status.
  *
- *  3. Batched host entry point (yu_csum_batch_host_uniform): the path that
- *     starts and ends in host memory (tun / link-layer buffers). It stages
- *     through library-owned pinned buffers and overlaps H2D copy, kernel and
- *     D2H copy on separate streams. Synchronous.
+ *  3. Batched host entry points (yu_csum_batch_host_uniform / _ragged / _iov,
+ *     and their _multi forms over several GPUs): the path that starts and
+ *     ends in host memory (tun / link-layer buffers). Batches up to 4 MiB are
+ *     read and answered in place over PCIe by the kernel (one launch, one
+ *     synchronisation); larger ones are staged through library-owned pinned
+ *     buffers with H2D copy, kernel and D2H copy overlapped on separate
+ *     streams. Synchronous.
  *
  * All arithmetic is unsigned integer. Results are bit-identical to the
  * reference Go code on the same bytes, including the reference's uint32
@@ -101,7 +104,9 @@ uint16_t yu_pseudo_header_checksum(uint32_t protocol,
 /* pkt_i = TCP segment (header incl. options, then data). out[i] = the value
  * sendTCP stores: ^TCP.CalculateChecksum(Checksum(data, pseudo), len) with
  * the checksum field taken as 0 — transport/tcp/connect.go:556-586,
- * header/tcp.go:165-186. Protocol 6. */
+ * header/tcp.go:165-186. Protocol 6. As in every segment sendTCP encodes,
+ * 20 <= DataOffset() <= len is required; other segments get an unspecified
+ * value (never a fault). */
 #define YU_MODE_TCP 2
 /* pkt_i = IPv4 datagram. out[i] = ^IPv4.CalculateChecksum() over
  * b[:IHL*4] (clamped to len) with the header-checksum field taken as 0 —

@@ -138,7 +138,11 @@ uint16_t or_packet(int mode, const uint8_t *pkt, uint64_t len,
     case OR_MODE_TCP: {
       /* transport/tcp/connect.go:556-586 (sendTCP) and :288-322 */
       size_t doff = (size_t)(pkt[12] >> 4) * 4;
-      memcpy(hdr, pkt, doff);
+      /* in contract 20 <= DataOffset <= len (every segment sendTCP encodes);
+       * outside it the value is unspecified, but never a read past the packet */
+      if (doff > len) doff = (size_t)len;
+      memset(hdr, 0, sizeof(hdr));
+      memcpy(hdr, pkt, doff < 20 && len >= 20 ? 20 : doff);
       hdr[16] = hdr[17] = 0; /* Encode: Checksum field zero value */
       uint16_t length = (uint16_t)doff;
       uint16_t xsum = batch_pseudo(6, addrs, initial_arr, initial, p);

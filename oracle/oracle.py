@@ -252,6 +252,7 @@ class _C:
 
 
 _c_singleton = None
+LIB_OPT_PATH = os.path.join(HERE, "build", "libcsum_oracle_opt.so")
 
 
 def C() -> _C:
@@ -259,3 +260,9 @@ def C() -> _C:
     if _c_singleton is None:
         _c_singleton = _C()
     return _c_singleton
+
+
+def C_opt() -> _C:
+    """The same C restatement built -O3 -march=x86-64-v3 (vectorised): the
+    "optimised CPU" baseline of SURVEY.md §8d. bench.py's cpu_baseline only."""
+    return _C(LIB_OPT_PATH)

@@ -247,3 +247,25 @@ def test_refexec_provenance(refexec):
         b = bytearray.fromhex(v["hex"])
         b[10:12] = b"\0\0"
         assert ~it.method("header", G.from_bytes(bytes(b), "IPv4"), "CalculateChecksum").v & 0xFFFF == v["want"]
+
+
+@pytest.mark.skipif(" avx2" not in open("/proc/cpuinfo").read(), reason="needs AVX2")
+def test_vectorised_build_agrees(oracle_c):
+    """The -O3 -march=x86-64-v3 build (bench's "optimised CPU" baseline) computes the
+    same results as the reference-faithful one."""
+    opt = O.C_opt()
+    rng = np.random.default_rng(5)
+    lens = rng.integers(60, 3000, size=2000)  # >= every mode's header (IHL / DataOffset <= 60)
+    offs = np.zeros(lens.size + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(offs[-1]) + 8, dtype=np.uint8)
+    data[offs[:-1].astype(np.int64) + 12] = rng.integers(5, 16, size=lens.size) << 4  # DataOffset 20..60
+    addrs = rng.integers(0, 256, size=8 * lens.size, dtype=np.uint8)
+    for mode in range(9):
+        a = oracle_c.batch(data, mode, offsets=offs, addrs=addrs)
+        b = opt.batch(data, mode, offsets=offs, addrs=addrs, threads=4)
+        assert np.array_equal(a, b), mode
+    big = rng.integers(0, 256, size=131073 + 140001, dtype=np.uint8)  # RAW past the uint32 wrap
+    bo = np.array([0, 131073, 131073 + 140001], np.uint64)
+    assert np.array_equal(oracle_c.batch(big, 0, offsets=bo, initial=0xFFFF),
+                          opt.batch(big, 0, offsets=bo, initial=0xFFFF))
