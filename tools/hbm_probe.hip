@@ -79,11 +79,12 @@ typedef void (*RK)(const uint4 *, uint64_t, uint32_t *);
 int main(int argc, char **argv) {
   const uint64_t bytes = argc > 1 ? strtoull(argv[1], 0, 10) : 1583349760ull;
   const int reps = 20, rounds = 3;
-  const int nbuf = 2;
+  // rotating copies: enough that the set exceeds the 256 MiB Infinity Cache
+  const int nbuf = argc > 2 ? atoi(argv[2]) : 2;
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   uint64_t n16 = bytes / 16;
-  uint4 *buf[nbuf];
+  std::vector<uint4 *> buf(nbuf);
   for (int b = 0; b < nbuf; ++b) {
     CK(hipMalloc(&buf[b], n16 * 16));
     fill<<<4096, 256>>>(buf[b], n16);
