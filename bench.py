@@ -206,6 +206,8 @@ def cpu_baseline(w: Workload, threads: int, budget_s: float):
                    f"1 thread: {r1:.3f} GiB/s, {n1} pass(es) over {s1} packets in {t1:.1f} s"),
         "value_1core": round(r1, 3),
         "cpu_work_s": round(t1 + tT * threads, 1),
+        "cpu_model": cpu_model(),
+        "host_cpus_visible": os.cpu_count(),
         **opt,
     }
 
@@ -268,6 +270,16 @@ def end_to_end(w: Workload, reps: int = 3):
         except Exception as e:  # reported, never fatal to the bench line
             res[f"pinned_{ndev}gpu_error"] = str(e)[:200]
     return res
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def host_threads() -> int:
