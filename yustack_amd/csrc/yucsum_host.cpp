@@ -122,6 +122,100 @@ struct Ctx {
 
 thread_local std::unique_ptr<Ctx> t_ctx[64];
 
+// Staging copies of pageable input. One thread's memcpy into pinned memory
+// runs at roughly half the PCIe rate, so a 32 MiB slice is split across a small
+// pool of persistent threads plus the caller. The pool serves one staging copy
+// at a time; a concurrent caller (another device's worker) copies on its own
+// thread instead of waiting. YU_HOST_COPY_THREADS sets the pool size (default
+// 7 helpers; 0 disables it).
+class CopyPool {
+ public:
+  static CopyPool &get() {
+    static CopyPool *p = new CopyPool();  // process lifetime: the helpers are detached
+    return *p;
+  }
+  // fn(i) for every i in [0, parts), on the helpers and the calling thread.
+  // Returns false (nothing run) when the pool is busy or empty.
+  bool run(int parts, const std::function<void(int)> &fn) {
+    if (nthreads_ == 0 || parts < 2) return false;
+    std::unique_lock<std::mutex> busy(run_m_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> l(m_);
+      job_ = &fn;
+      parts_ = parts;
+      next_ = 0;
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(m_);
+    done_cv_.wait(l, [&] { return done_ == parts_; });
+    job_ = nullptr;
+    return true;
+  }
+  int threads() const { return nthreads_; }
+
+ private:
+  CopyPool() {
+    const char *e = getenv("YU_HOST_COPY_THREADS");
+    nthreads_ = e && *e ? atoi(e) : 7;
+    if (nthreads_ < 0) nthreads_ = 0;
+    if (nthreads_ > 64) nthreads_ = 64;
+    for (int i = 0; i < nthreads_; ++i) std::thread([this] { loop(); }).detach();
+  }
+  // Claims parts of the current job until none are left.
+  void work() {
+    for (;;) {
+      int i;
+      const std::function<void(int)> *f;
+      {
+        std::lock_guard<std::mutex> l(m_);
+        if (!job_ || next_ >= parts_) return;
+        i = next_++;
+        f = job_;
+      }
+      (*f)(i);
+      std::lock_guard<std::mutex> l(m_);
+      if (++done_ == parts_) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  int nthreads_ = 0;
+  std::mutex run_m_, m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)> *job_ = nullptr;
+  int parts_ = 0, next_ = 0, done_ = 0;
+  uint64_t gen_ = 0;
+};
+
+constexpr uint64_t kParCopyMin = 1ull << 20;  // below this one memcpy is faster
+
+void stage_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
+  CopyPool &pool = CopyPool::get();
+  if (n >= 2 * kParCopyMin) {
+    const uint64_t parts = std::min<uint64_t>((uint64_t)pool.threads() + 1, n / kParCopyMin);
+    const uint64_t chunk = ((n + parts - 1) / parts + 63) & ~63ull;
+    if (pool.run((int)parts, [&](int i) {
+          const uint64_t a = (uint64_t)i * chunk;
+          if (a < n) memcpy(dst + a, src + a, std::min(chunk, n - a));
+        }))
+      return;
+  }
+  memcpy(dst, src, n);
+}
+
 bool is_pinned(const void *p) {
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -290,7 +384,7 @@ struct UniformLayout {
     const uint8_t *src = h_data + first * stride;
     const uint64_t b = bytes(first, cnt);
     if (pin_in || !b) return src;
-    memcpy(x.h_data, src, b);
+    stage_copy(x.h_data, src, b);
     return x.h_data;
   }
   int launch(const uint8_t *d, const uint64_t *, uint64_t cnt, const uint16_t *d_init,
@@ -331,7 +425,7 @@ struct RaggedLayout {
     for (uint64_t i = 0; i <= cnt; ++i) x.h_off[i] = off[first + i] - o0;
     const uint64_t b = bytes(first, cnt);
     if (pin_in || !b) return h_data + o0;
-    memcpy(x.h_data, h_data + o0, b);
+    stage_copy(x.h_data, h_data + o0, b);
     return x.h_data;
   }
   int launch(const uint8_t *d, const uint64_t *d_off, uint64_t cnt, const uint16_t *d_init,
@@ -367,12 +461,30 @@ struct IovLayout {
     uint64_t o = 0;
     for (uint64_t i = 0; i < cnt; ++i) {
       x.h_off[i] = o;
-      for (uint64_t v = first_iov[first + i]; v < first_iov[first + i + 1]; ++v) {
-        if (iov[v].len) memcpy(x.h_data + o, iov[v].base, iov[v].len);
-        o += iov[v].len;
-      }
+      o += plen(first + i);
     }
     x.h_off[cnt] = o;
+    // gather packets [a, b) of the slice into their staging offsets
+    auto gather = [&](uint64_t a, uint64_t b) {
+      for (uint64_t i = a; i < b; ++i) {
+        uint64_t d = x.h_off[i];
+        for (uint64_t v = first_iov[first + i]; v < first_iov[first + i + 1]; ++v) {
+          if (iov[v].len) memcpy(x.h_data + d, iov[v].base, iov[v].len);
+          d += iov[v].len;
+        }
+      }
+    };
+    CopyPool &pool = CopyPool::get();
+    const uint64_t parts = std::min<uint64_t>((uint64_t)pool.threads() + 1, o / kParCopyMin);
+    if (parts >= 2 && cnt >= parts) {
+      const uint64_t per = (cnt + parts - 1) / parts;
+      if (pool.run((int)parts, [&](int i) {
+            const uint64_t a = (uint64_t)i * per;
+            gather(std::min(a, cnt), std::min(a + per, cnt));
+          }))
+        return x.h_data;
+    }
+    gather(0, cnt);
     return x.h_data;
   }
   int launch(const uint8_t *d, const uint64_t *d_off, uint64_t cnt, const uint16_t *d_init,
