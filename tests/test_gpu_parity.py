@@ -531,3 +531,39 @@ def test_refexec_vectors_on_gpu(dev):
         d = np.full(v["len"], v["fill"], np.uint8)
         got = batch.checksum_uniform(_to(dev, d), v["len"], v["len"], 1, "raw", initial=v["initial"])
         assert int(got.cpu().numpy()[0]) == v["want"], v
+
+
+def test_host_paths_concurrent_callers(dev, oracle_c):
+    """The host entry points are thread-safe (include/yucsum.h): several threads,
+    each with its own staging context, call the pipelined, direct and multi-device
+    paths at once (the copy pool serves one of them at a time, the rest copy on
+    their own threads), every result bit-exact."""
+    import threading
+    rng = np.random.default_rng(37)
+    jobs = []
+    for k in range(6):
+        n, L = (20000, 1500) if k % 3 == 0 else ((300, 1500) if k % 3 == 1 else (5000, 700))
+        host = _rand(rng, n * L)
+        host[12::L] = 0x50
+        addrs = _rand(rng, 8 * n)
+        want = oracle_c.batch(host, O.MODE_TCP, stride=L, length=L, n=n, addrs=addrs, threads=4)
+        jobs.append((host, L, n, addrs, want, [0, 0] if k % 3 == 2 else 0))
+    errors = []
+
+    def worker(job):
+        host, L, n, addrs, want, devs = job
+        try:
+            for _ in range(3):
+                got = batch.checksum_host_uniform(host, L, L, n, "tcp", addrs=addrs, device=devs)
+                if not np.array_equal(got, want):
+                    errors.append(("mismatch", n, L))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(j,)) for j in jobs]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not any(t.is_alive() for t in ts), "host call hung"
+    assert not errors, errors
