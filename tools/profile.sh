@@ -9,10 +9,13 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-for cfg in ${CFGS:-3 2 4 6}; do
+for cfg in ${CFGS:-3 2 4 6 7}; do
+  # 5 warm-up + 30 timed launches; tools/trace_summary.py <csv> 30 averages the same
+  # 30 launches bench.py's HIP events time (the stats CSV also counts the warm-up)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c$cfg" -o run -- \
-    python3 "$ROOT/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --no-extra --no-e2e \
+    python3 "$ROOT/bench.py" --config $cfg --steps 30 --warmup 5 --no-cpu-baseline --no-extra --no-e2e \
     > "$OUT/bench_c${cfg}_under_trace.json"
+  [ -n "${NO_PMC:-}" ] && continue
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_${ctr}_c$cfg" -o run -- \
       python3 "$ROOT/bench.py" --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-extra --no-e2e \
