@@ -567,3 +567,55 @@ def test_host_paths_concurrent_callers(dev, oracle_c):
         t.join(120)
     assert not any(t.is_alive() for t in ts), "host call hung"
     assert not errors, errors
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_full_size_fill_then_verify_round_trip(dev):
+    """Size-independent property at BASELINE config 3 and 4 sizes: writing the TX
+    field in place (yu_csum_fill_*, SetChecksum semantics) and then verifying the same
+    bytes (checker semantics) accepts every packet; flipping one bit in a chosen set
+    of packets rejects exactly that set."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(99)
+    n, L = 1 << 20, 1500  # config 3
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
+    d.view(n, L)[:, 12] = 0x50
+    a = torch.randint(0, 256, (8 * n,), dtype=torch.uint8, device=dev, generator=g)
+    batch.checksum_uniform(d, L, L, n, "tcp", addrs=a, fill=True)
+    ok = batch.verified(batch.checksum_uniform(d, L, L, n, "verify_tcp", addrs=a))
+    assert bool(ok.all())
+    bad = torch.randperm(n, device=dev, generator=g)[:1000]
+    pos = bad * L + 20 + torch.randint(0, L - 20, (1000,), device=dev, generator=g)
+    d[pos] ^= 0x04
+    ok = batch.verified(batch.checksum_uniform(d, L, L, n, "verify_tcp", addrs=a))
+    mask = torch.ones(n, dtype=torch.bool, device=dev)
+    mask[bad] = False
+    assert torch.equal(ok, mask)
+    del d
+    # config 4 shape, UDP datagrams packed back to back (4-aligned offsets for fill)
+    rng = np.random.default_rng(4)
+    lens = (rng.integers(64, 9001, size=n) + 3) & ~3
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    r = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device=dev, generator=g)
+    o = _to(dev, offs)
+    batch.checksum_ragged(r, o, "udp", addrs=a, fill=True)
+    ok = batch.verified(batch.checksum_ragged(r, o, "verify_udp", addrs=a))
+    assert bool(ok.all())
+
+
+def test_raw_packets_beyond_2GiB(dev, oracle_c):
+    """RAW packets longer than 2 GiB (buffer-descriptor extents are 2 GiB; windows and
+    tiles re-base) with the reference's uint32 wrap, uniform and ragged, against the
+    oracle."""
+    big = (5 << 29) + 3  # 2.5 GiB + 3, odd
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    d = torch.randint(0, 256, (big + 1000,), dtype=torch.uint8, device=dev, generator=g)
+    host = d.cpu().numpy()
+    got = batch.checksum_uniform(d, big, big, 1, "raw", initial=0x1234).cpu().numpy()
+    assert int(got[0]) == oracle_c.checksum(host[:big].tobytes(), 0x1234)
+    offs = np.array([0, 17, 17 + big, 17 + big + 980], np.int64)
+    got = batch.checksum_ragged(d, _to(dev, offs), "raw", initial=0xFFFF).cpu().numpy()
+    want = oracle_c.batch(host, O.MODE_RAW, offsets=offs.astype(np.uint64), initial=0xFFFF)
+    assert np.array_equal(got, want)
