@@ -619,3 +619,22 @@ def test_raw_packets_beyond_2GiB(dev, oracle_c):
     got = batch.checksum_ragged(d, _to(dev, offs), "raw", initial=0xFFFF).cpu().numpy()
     want = oracle_c.batch(host, O.MODE_RAW, offsets=offs.astype(np.uint64), initial=0xFFFF)
     assert np.array_equal(got, want)
+
+
+def test_more_than_2pow32_packets(dev):
+    """A batch of 2^32 + 5 one-byte packets (stride 1): packet indices, side-array and
+    result offsets past 32 bits. Checksum of one odd byte b with initial i is
+    fold(i + (b << 8)) (checksum/checksum.go:8-11,17); checked on the device in
+    slices against that closed form."""
+    n = (1 << 32) + 5
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    d = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
+    out = batch.checksum_uniform(d, 1, 1, n, "raw", initial=0xFFF0)
+    step = 1 << 28
+    for a in range(0, n, step):
+        b = min(n, a + step)
+        x = (d[a:b].to(torch.int32) << 8) + 0xFFF0
+        x = (x & 0xFFFF) + (x >> 16)
+        assert torch.equal(out[a:b].view(torch.int16).to(torch.int32) & 0xFFFF, x), a
+    assert int(out[-1].view(torch.int16)) & 0xFFFF == int(x[-1])
