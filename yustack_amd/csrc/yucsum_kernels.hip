@@ -45,14 +45,21 @@
 // loads in flight while the current step is summed (software pipelining).
 //
 // Work mapping (wave64-first, not a warp tiling):
+//   k_tiny<G>: uniform, packets <= 16G bytes, 4-aligned, no junk bytes: a wave
+//     step covers 64 packets, each load instruction one contiguous KiB, and a
+//     cross-lane transpose lets every lane finish one packet (BASELINE config 2).
 //   k_small<G, U>: uniform stride, packet span <= G*U*16 bytes. A wave holds
 //     64/G packets per step; each group of G lanes loads its packet window in
-//     U dwordx4 loads per lane (1 KiB per wave-instruction), reduces with
-//     log2(G) DPP adds and its last lane finishes the packet.
-//   k_loop<U, BE>: one wave per packet, looping over 64*U*16-byte windows, for
-//     ragged (tun-style, any alignment) batches and uniform packets > 4 KiB.
-//   Both are grid-stride kernels; the grid is sized per CU and over-subscribed
-//   (see blocks_per_cu).
+//     U dwordx4 loads per lane, reduces with log2(G) DPP adds and its last
+//     lane finishes the packet (config 3: k_small<16,6>).
+//   k_seg<U, NT, K>: ragged (tun-style, any alignment) batches and VERIFY_RX:
+//     a segmented sum over the byte stream of 64 consecutive packets per wave,
+//     U KiB tiles, packet sums as prefix differences (config 4, tun RX).
+//   k_rag<G, U>: ragged IPv4 header-only modes (<= 60 bytes of each packet).
+//   k_loop<U, BE>: one wave per packet, for uniform packets > 4 KiB.
+//   All are grid-stride kernels; the grid is sized per CU and over-subscribed
+//   (see blocks_per_cu), except that k_seg narrows it for small packets
+//   (seg_waves).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
