@@ -638,3 +638,23 @@ def test_more_than_2pow32_packets(dev):
         x = (x & 0xFFFF) + (x >> 16)
         assert torch.equal(out[a:b].view(torch.int16).to(torch.int32) & 0xFFFF, x), a
     assert int(out[-1].view(torch.int16)) & 0xFFFF == int(x[-1])
+
+
+def test_direct_path_back_to_back_bursts(dev, oracle_c):
+    """Hundreds of consecutive small bursts through the direct host path (results
+    read back by polling a GPU-written completion flag), each with fresh bytes and a
+    changing size, so a result read before it landed would show as a mismatch."""
+    rng = np.random.default_rng(41)
+    pin = torch.empty(64 * 1500, dtype=torch.uint8).pin_memory()
+    for it in range(400):
+        n = int(rng.integers(1, 65))
+        L = int(rng.choice([40, 64, 576, 1500]))
+        host = _rand(rng, n * L)
+        addrs = _rand(rng, 8 * n)
+        want = oracle_c.batch(host, O.MODE_UDP, stride=L, length=L, n=n, addrs=addrs)
+        if it % 2:
+            pin[: n * L].copy_(torch.from_numpy(host))
+            got = batch.checksum_host_uniform(pin[: n * L], L, L, n, "udp", addrs=addrs)
+        else:
+            got = batch.checksum_host_uniform(host, L, L, n, "udp", addrs=addrs)
+        assert np.array_equal(got, want), (it, n, L)

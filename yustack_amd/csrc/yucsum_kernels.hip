@@ -69,6 +69,7 @@
 #include <atomic>
 
 #include "yucsum.h"
+#include "yucsum_internal.h"
 
 namespace {
 
@@ -1592,7 +1593,21 @@ int batch_ragged(const uint8_t *data, uint8_t *fill, const uint64_t *offsets,
   return launch(pick_ragged(mode), A, (hipStream_t)stream);
 }
 
+// Completion signal for the host path's direct mode (yucsum_internal.h):
+// stored after the work before it on the stream, with system-scope release,
+// into coherent pinned host memory.
+__global__ void k_signal(volatile uint32_t *flag, uint32_t value) {
+  __threadfence_system();
+  *flag = value;
+  __threadfence_system();
+}
+
 }  // namespace
+
+int yu_internal_signal(uint32_t *flag, uint32_t value, void *stream) {
+  hipLaunchKernelGGL(k_signal, dim3(1), dim3(1), 0, (hipStream_t)stream, flag, value);
+  return hip_status(hipGetLastError());
+}
 
 extern "C" {
 
