@@ -147,7 +147,7 @@ def test_python_front_end_refuses_cpu_tensors():
     (1536, 1536, "raw", 1, "k_small<32,4>"),     # 1539 > 1536
     (9000, 9000, "raw", 0, "k_loop<4,LE>"),
     (200000, 200000, "raw", 0, "k_loop<4,BE>"),  # > 131072: exact uint32 wrap path
-    (1500, 1500, "ipv4", 0, "k_small<4,1>"),     # only the <= 60-byte header is read
+    (1500, 1500, "ipv4", 0, "k_hdr"),            # only the <= 60-byte header is read
     (20, 20, "udp", 3, "k_small<4,1>"),
     (62, 62, "raw", 1, "k_small<8,1>"),      # 65 > 64
 ])

@@ -658,3 +658,27 @@ def test_direct_path_back_to_back_bursts(dev, oracle_c):
         else:
             got = batch.checksum_host_uniform(host, L, L, n, "udp", addrs=addrs)
         assert np.array_equal(got, want), (it, n, L)
+
+
+def test_fill_ragged_ipv4_headers(dev, oracle_c):
+    """Ragged IPv4 TX in place (k_hdr): the header field written big-endian equals
+    the oracle's value, and the filled headers verify (checker.IPv4)."""
+    rng = np.random.default_rng(43)
+    n = 3000
+    lens = (rng.integers(20, 1501, size=n) + 3) & ~3
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    blob = _rand(rng, int(offs[-1]))
+    for i in range(n):
+        s = int(offs[i])
+        ihl = int(rng.integers(5, 16))
+        blob[s] = 0x40 | (ihl if ihl * 4 <= lens[i] else 5)
+    want = oracle_c.batch(blob, O.MODE_IPV4, offsets=offs)
+    d = _to(dev, blob)
+    got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), "ipv4", fill=True).cpu().numpy()
+    assert np.array_equal(got, want)
+    filled = d.cpu().numpy()
+    fields = (filled[offs[:-1].astype(np.int64) + 10].astype(np.uint16) << 8) | filled[offs[:-1].astype(np.int64) + 11]
+    assert np.array_equal(fields, want)
+    v = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), "verify_ipv4")
+    assert bool(batch.verified(v).all())

@@ -31,6 +31,17 @@ __global__ void fill(uint8_t *p, uint64_t n, uint32_t seed) {
   }
 }
 
+// IPv4 version/IHL byte 0x45 at every packet start (kbench config 12: real headers)
+__global__ void set_ihl(uint8_t *p, const uint64_t *off, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (uint64_t)gridDim.x * blockDim.x) p[off[i]] = 0x45;
+}
+
+__global__ void set_ihl_stride(uint8_t *p, uint64_t stride, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (uint64_t)gridDim.x * blockDim.x) p[i * stride] = 0x45;
+}
+
 static void on_segv(int sig) {
   void *bt[64];
   const int k = backtrace(bt, 64);
@@ -64,12 +75,16 @@ int main(int argc, char **argv) {
     uint64_t *d_off = nullptr;
     if (cfg == 2) { L = 64; mode = YU_MODE_RAW; bytes = n * L; alg = bytes + 4 * n; }
     if (cfg == 3) { L = 1500; mode = YU_MODE_TCP; bytes = n * L; alg = bytes + 10 * n; }
-    if (cfg >= 4 && cfg <= 10) {
+    // 13: uniform 1M x 1500 B IPv4 datagrams, header checksum only (20-B headers)
+    if (cfg == 13) { L = 1500; mode = YU_MODE_IPV4; bytes = n * L; alg = 20 * n + 2 * n; }
+    if (cfg >= 4 && cfg <= 12) {
       // 4: BASELINE config 4 (U{64..9000}); 5: tun-like U{64..1500}; 6: U{40..200}
       // (RAW + initial); 7: U{64..1500} TCP segments, 8: U{40..200} UDP (TX kinds, addrs)
       // 9: U{40..600}, 10: U{40..1000} (RAW + initial): small-grid crossover
       const int lo = (cfg == 4 || cfg == 5 || cfg == 7) ? 64 : 40;
-      const int hi = cfg == 4 ? 9000 : ((cfg == 5 || cfg == 7) ? 1500 : (cfg == 9 ? 600 : (cfg == 10 ? 1000 : 200)));
+      const int hi = cfg == 4 ? 9000 : ((cfg == 5 || cfg == 7 || cfg == 11 || cfg == 12) ? 1500 : (cfg == 9 ? 600 : (cfg == 10 ? 1000 : 200)));
+      // 11: U{40..1500} IPv4 datagrams, header checksum only (k_rag)
+      if (cfg == 11 || cfg == 12) mode = YU_MODE_IPV4;  // 12: IHL 5 in every header
       if (cfg == 7) mode = YU_MODE_TCP;
       if (cfg == 8) mode = YU_MODE_UDP;
       std::mt19937_64 rng(4);
@@ -78,6 +93,7 @@ int main(int argc, char **argv) {
       for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + d(rng);
       bytes = off[n];
       alg = bytes + 8 * (n + 1) + (mode == YU_MODE_RAW ? 4 : 10) * n;
+      if (mode == YU_MODE_IPV4) alg = 40 * n + 8 * (n + 1) + 2 * n;  // ~mean IHL*4 of random headers
       CK(hipMalloc(&d_off, (n + 1) * 8));
       CK(hipMemcpy(d_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
     }
@@ -86,10 +102,12 @@ int main(int argc, char **argv) {
     for (int r = 0; r < R; ++r) {
       CK(hipMalloc(&bufs[r], bytes + 64));
       fill<<<4096, 256>>>(bufs[r], bytes + 64, 100 + r);
+      if (cfg == 12) set_ihl<<<1024, 256>>>(bufs[r], d_off, n);
+      if (cfg == 13) set_ihl_stride<<<1024, 256>>>(bufs[r], L, n);
     }
     CK(hipDeviceSynchronize());
     auto launch = [&](int k) {
-      const bool tx = mode != YU_MODE_RAW;
+      const bool tx = mode != YU_MODE_RAW && mode != YU_MODE_IPV4;
       int rc = d_off ? yu_csum_batch_ragged(bufs[k % R], d_off, n, mode, tx ? nullptr : init, 0,
                                             tx ? addrs : nullptr, out, nullptr)
                      : yu_csum_batch_uniform(bufs[k % R], L, L, n, mode, cfg == 2 ? init : nullptr, 0,
