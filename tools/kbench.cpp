@@ -97,6 +97,9 @@ int main(int argc, char **argv) {
       CK(hipMalloc(&d_off, (n + 1) * 8));
       CK(hipMemcpy(d_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
     }
+    // KB_MODE=<0..8> overrides the mode (perf matrix over all modes); addrs for
+    // the pseudo-header modes, initial for RAW, nothing for the others
+    if (getenv("KB_MODE")) mode = atoi(getenv("KB_MODE"));
     int R = (int)((2ull << 30) / bytes + 1);
     std::vector<uint8_t *> bufs(R);
     for (int r = 0; r < R; ++r) {
@@ -107,11 +110,13 @@ int main(int argc, char **argv) {
     }
     CK(hipDeviceSynchronize());
     auto launch = [&](int k) {
-      const bool tx = mode != YU_MODE_RAW && mode != YU_MODE_IPV4;
-      int rc = d_off ? yu_csum_batch_ragged(bufs[k % R], d_off, n, mode, tx ? nullptr : init, 0,
-                                            tx ? addrs : nullptr, out, nullptr)
-                     : yu_csum_batch_uniform(bufs[k % R], L, L, n, mode, cfg == 2 ? init : nullptr, 0,
-                                             cfg == 3 ? addrs : nullptr, out, nullptr);
+      const bool ph = mode == YU_MODE_UDP || mode == YU_MODE_TCP || mode == YU_MODE_VERIFY_TCP ||
+                      mode == YU_MODE_VERIFY_UDP;
+      const uint16_t *ia = mode == YU_MODE_RAW ? init : nullptr;
+      int rc = d_off ? yu_csum_batch_ragged(bufs[k % R], d_off, n, mode, ia, 0, ph ? addrs : nullptr,
+                                            out, nullptr)
+                     : yu_csum_batch_uniform(bufs[k % R], L, L, n, mode, ia, 0, ph ? addrs : nullptr, out,
+                                             nullptr);
       if (rc) { fprintf(stderr, "rc %d\n", rc); exit(1); }
     };
     for (int r = 0; r < rounds; ++r) {
