@@ -140,7 +140,8 @@ def test_python_front_end_refuses_cpu_tensors():
 
 @pytest.mark.parametrize("stride,length,mode,align,want", [
     (64, 64, "raw", 0, "k_tiny<4>"),
-    (64, 64, "udp", 0, "k_small<4,1>"),      # TX field: junk -> k_small
+    (64, 64, "udp", 0, "k_tiny<4>"),         # TX field masked in k_tiny
+    (64, 64, "udp", 1, "k_small<8,1>"),      # unaligned start: head junk -> k_small (67 > 64)
     (128, 120, "verify_tcp", 0, "k_tiny<8>"),
     (1500, 1500, "tcp", 0, "k_small<16,6>"),
     (1500, 1500, "tcp", 2, "k_small<16,6>"),     # 1503 still fits 1536

@@ -241,11 +241,12 @@ def test_raw_uint32_wrap(dev, oracle_c):
     assert got[0] == 65534  # the reference's wrapped value (exact sum would give 65535)
 
 
+@pytest.mark.parametrize("L", [1500, 124, 64, 20])  # k_small / k_hdr, and k_tiny<8>, k_tiny<4>
 @pytest.mark.parametrize("mode", [O.MODE_UDP, O.MODE_TCP, O.MODE_IPV4, O.MODE_ICMP])
-def test_fill_in_place(dev, oracle_c, mode):
+def test_fill_in_place(dev, oracle_c, mode, L):
     """fill=True writes the TX field (SetChecksum); re-verifying gives 0/0xFFFF."""
-    rng = np.random.default_rng(77 + mode)
-    n, L = 333, 1500
+    rng = np.random.default_rng(77 + mode + L)
+    n = 333
     host = _rand(rng, n * L)
     pk = host.reshape(n, L)
     if mode == O.MODE_TCP:

@@ -503,7 +503,8 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
 
 // ---------------------------------------------------------------------
 // k_tiny<G, NT>: uniform stride, packets of <= 16G bytes starting 4-byte
-// aligned, in the modes without junk bytes (RAW, VERIFY_TCP, VERIFY_UDP).
+// aligned: RAW, the TX modes UDP / TCP / ICMP (field masked in place) and
+// VERIFY_TCP / VERIFY_UDP — every mode without a per-packet header walk.
 // For tiny packets k_small spends a whole per-packet epilogue on every 1 KiB
 // loaded; here a wave step covers 64 packets (G KiB): group g (G lanes) loads
 // chunk j of G packets (slot k holds packet pb + (64/G)k + g, so each load
@@ -557,6 +558,14 @@ __global__ __launch_bounds__(256) void k_tiny(BatchArgs A) {
   const int lim[4] = {F, F - 4, F - 8, F - 12};
   const uint32_t tm = (1u << (8u * (E & 3u))) - 1u;
   const bool full = A.uf != 0;  // every chunk of every packet is whole
+  // TX modes: Encode leaves the checksum field 0. Starts are 4-aligned and the
+  // field offset is even, so the field is 16 bits of one dword: chunk f/16,
+  // dword (f%16)/4 — masked in the lanes that load that chunk.
+  const uint32_t f = mode_field(A.mode);
+  const uint32_t fm = (mode_is_tx(A.mode) && j == f / 16u) ? ~(0xFFFFu << (8u * (f & 3u))) : ~0u;
+  const uint32_t fd = (f >> 2) & 3u;
+  const uint4 m4 = make_uint4(fd == 0 ? fm : ~0u, fd == 1 ? fm : ~0u, fd == 2 ? fm : ~0u,
+                              fd == 3 ? fm : ~0u);
 
   uint64_t pb = wave * 64u;
   if (pb >= A.n) return;
@@ -571,13 +580,16 @@ __global__ __launch_bounds__(256) void k_tiny(BatchArgs A) {
     uint32_t mine = 0;
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-      uint32_t acc = full ? sum_full<false>(it.c[k], 0u, 0u)
-                          : sum_masked<false>(it.c[k], 16 * (int)j, lim, tm, 0u, 0u);
+      const uint4 c = make_uint4(it.c[k].x & m4.x, it.c[k].y & m4.y, it.c[k].z & m4.z,
+                                 it.c[k].w & m4.w);
+      uint32_t acc = full ? sum_full<false>(c, 0u, 0u)
+                          : sum_masked<false>(c, 16 * (int)j, lim, tm, 0u, 0u);
       acc = bcast_last<G>(group_total<G>(acc), lane);
       mine = (j == (uint32_t)k) ? acc : mine;
     }
     const uint64_t pf = pb + GPW * j + g;
-    if (pf < A.n) finish_packet(A, pf, le_to_be(mine, 0u), E, it.sd, nullptr, E);
+    if (pf < A.n)
+      finish_packet(A, pf, le_to_be(mine, 0u), E, it.sd, A.fill ? A.fill + pf * A.stride : nullptr, E);
     if (!more) break;
     it = nx;
     pb = pn;
@@ -1506,8 +1518,7 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
     return span <= v.window && v.ppw * stride + v.window < kOOB;
   };
   // k_tiny: no junk bytes (4-aligned starts, no TX field, no IPv4 header walk)
-  const bool tiny_ok = aligned4 && (mode == YU_MODE_RAW || mode == YU_MODE_VERIFY_TCP ||
-                                    mode == YU_MODE_VERIFY_UDP);
+  const bool tiny_ok = aligned4 && !mode_is_ipv4(mode) && mode != YU_MODE_VERIFY_RX;
   if (mode == YU_MODE_VERIFY_RX) return pick_ragged(mode);
   // IPv4 header-only modes: one lane per packet (1M x 1500-B datagrams:
   // 29.9 us vs 36.9 with k_small<4,1>, kbench 13)
