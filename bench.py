@@ -63,6 +63,11 @@ class Workload:
             nbytes = n * self.L
             self.side = 2 * n  # uint16 initial
             self.name = "config2: 1M x 64-B UDP payloads, Checksum(payload, pseudo) per packet"
+        elif cfg == 8:  # config 2 as whole UDP datagrams: 8-B header + 64-B payload, sendUDP field
+            self.mode, self.L = batch.UDP, 72
+            nbytes = n * self.L
+            self.side = 8 * n  # addrs
+            self.name = "config2-udp: 1M x (8-B UDP header + 64-B payload), sendUDP field value"
         elif cfg == 3:  # 1M x 1500-B TCP segments, (src,dst) side array
             self.mode, self.L = batch.TCP, 1500
             nbytes = n * self.L
@@ -107,7 +112,7 @@ class Workload:
         if cfg == 2 or cfg == 4:
             self.initial_arr = torch.randint(0, 65536, (n,), dtype=torch.int32, device=dev,
                                              generator=g).to(torch.uint16)
-        if cfg == 3:
+        if cfg in (3, 8):
             self.addrs = torch.randint(0, 256, (8 * n,), dtype=torch.uint8, device=dev, generator=g)
         self.out = torch.empty(n, dtype=torch.uint16, device=dev)
         if self.offsets is not None:  # validate once; the timed launches skip the check
@@ -295,7 +300,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 6, 7])
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 6, 7, 8])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip configs 2/4 side measurements")
     ap.add_argument("--cpu-budget", type=float, default=6.0, help="wall seconds for the CPU baseline")
@@ -354,7 +359,7 @@ def main():
             "workload": w.name,
             "packets_per_gpu": w.n,
             "packet_bytes": w.L if w.L else "U{64..9000}",
-            "mode": {0: "raw", 2: "tcp", 8: "verify_rx"}.get(w.mode, str(w.mode)),
+            "mode": {0: "raw", 1: "udp", 2: "tcp", 8: "verify_rx"}.get(w.mode, str(w.mode)),
             "algorithmic_bytes_per_step_per_gpu": w.bytes,
             "rotating_batches": w.R,
             "kernel": w.kernel_name(),
@@ -375,7 +380,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_extra:
         extra = {}
-        for c in (2, 3, 4, 6, 7):
+        for c in (2, 8, 3, 4, 6, 7):
             if c == args.config:
                 continue
             wc = Workload(c, dev, seed=77 + c)
