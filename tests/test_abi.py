@@ -142,7 +142,12 @@ def test_python_front_end_refuses_cpu_tensors():
     (64, 64, "raw", 0, "k_tiny<4>"),
     (64, 64, "udp", 0, "k_tiny<4>"),         # TX field masked in k_tiny
     (64, 64, "udp", 1, "k_small<8,1>"),      # unaligned start: head junk -> k_small (67 > 64)
-    (128, 120, "verify_tcp", 0, "k_tiny<8>"),
+    (128, 120, "verify_tcp", 0, "k_tiny<8>"),   # > 112 bytes: every k_tiny<8> lane loads
+    (128, 100, "raw", 0, "k_lane<8>"),          # 64 whole strides per wave step in LDS
+    (100, 100, "tcp", 0, "k_lane<7>"),
+    (72, 72, "udp", 0, "k_lane<5>"),            # sendUDP datagram: 8-B header + 64-B payload
+    (72, 70, "raw", 2, "k_small<8,1>"),         # unaligned: no k_lane
+    (136, 128, "raw", 0, "k_tiny<8>"),          # stride > 128: no k_lane
     (1500, 1500, "tcp", 0, "k_small<16,6>"),
     (1500, 1500, "tcp", 2, "k_small<16,6>"),     # 1503 still fits 1536
     (1536, 1536, "raw", 1, "k_small<32,4>"),     # 1539 > 1536

@@ -77,6 +77,38 @@ def test_transport_uniform(dev, oracle_c, mode, length):
         assert np.array_equal(got, want), (mode, length, base_off, stride_pad)
 
 
+@pytest.mark.parametrize("mode", [O.MODE_RAW, O.MODE_UDP, O.MODE_TCP, O.MODE_ICMP,
+                                  O.MODE_VERIFY_TCP, O.MODE_VERIFY_UDP])
+def test_lane_kernel_shapes(dev, oracle_c, mode):
+    """k_lane (65..112-byte uniform packets, strides to 128): tails of 1-3 bytes,
+    gaps between packets (stride > len), every LDS read width, partial last wave
+    steps, and the TX field; k_tiny<8> takes over above 112 bytes."""
+    rng = np.random.default_rng(3000 + mode)
+    use_addrs = mode in (O.MODE_UDP, O.MODE_TCP, O.MODE_VERIFY_TCP, O.MODE_VERIFY_UDP)
+    seen = set()
+    for length, stride in ((65, 68), (66, 68), (67, 68), (68, 68), (71, 72), (72, 72), (72, 80),
+                           (80, 80), (81, 96), (96, 96), (100, 100), (104, 104), (112, 112),
+                           (100, 128), (112, 128), (127, 128), (128, 128)):
+        seen.add(batch.variant(stride, length, mode, 0))
+        for n in (1, 63, 64, 65, 1000):
+            got, want = _uniform_case(dev, oracle_c, rng, length, stride, n, mode,
+                                      use_addrs=use_addrs, use_init_arr=not use_addrs)
+            assert np.array_equal(got, want), (mode, length, stride, n)
+    assert seen == {"k_lane<5>", "k_lane<6>", "k_lane<7>", "k_lane<8>", "k_tiny<8>"}, seen
+
+
+def test_lane_kernel_grid_stride(dev, oracle_c):
+    """More packets than one pass of the k_lane grid: 1.3M x 72-B UDP datagrams."""
+    rng = np.random.default_rng(5)
+    n, L = 1_300_000, 72
+    assert batch.variant(L, L, "udp", 0) == "k_lane<5>"
+    host = _rand(rng, n * L)
+    addrs = _rand(rng, 8 * n)
+    got = batch.checksum_uniform(_to(dev, host), L, L, n, "udp", addrs=_to(dev, addrs)).cpu().numpy()
+    want = oracle_c.batch(host, O.MODE_UDP, stride=L, length=L, n=n, addrs=addrs)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("mode", [O.MODE_IPV4, O.MODE_VERIFY_IPV4, O.MODE_ICMP])
 @pytest.mark.parametrize("length", [4, 20, 21, 24, 60, 61, 64, 100, 1500, 1501])
 def test_ipv4_icmp_uniform(dev, oracle_c, mode, length):
@@ -241,7 +273,7 @@ def test_raw_uint32_wrap(dev, oracle_c):
     assert got[0] == 65534  # the reference's wrapped value (exact sum would give 65535)
 
 
-@pytest.mark.parametrize("L", [1500, 124, 64, 20])  # k_small / k_hdr, and k_tiny<8>, k_tiny<4>
+@pytest.mark.parametrize("L", [1500, 124, 100, 72, 64, 20])  # k_small / k_hdr, k_tiny<8>, k_lane<7>, k_lane<5>, k_tiny<4>
 @pytest.mark.parametrize("mode", [O.MODE_UDP, O.MODE_TCP, O.MODE_IPV4, O.MODE_ICMP])
 def test_fill_in_place(dev, oracle_c, mode, L):
     """fill=True writes the TX field (SetChecksum); re-verifying gives 0/0xFFFF."""

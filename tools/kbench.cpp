@@ -3,7 +3,7 @@
 // the loop, for quick kernel A/B work and rocprofv3 runs.
 //
 // build: hipcc -O2 --offload-arch=gfx950 -I include tools/kbench.cpp -o tools/kbench -L yustack_amd -lyucsum -Wl,-rpath,'$ORIGIN/../yustack_amd'
-// run:   tools/kbench [config...]   (default 2 3 4)
+// run:   tools/kbench [config...]   (default 2 3 4; 14 reads KB_LEN)
 #include <hip/hip_runtime.h>
 #include <execinfo.h>
 #include <signal.h>
@@ -77,6 +77,13 @@ int main(int argc, char **argv) {
     if (cfg == 3) { L = 1500; mode = YU_MODE_TCP; bytes = n * L; alg = bytes + 10 * n; }
     // 13: uniform 1M x 1500 B IPv4 datagrams, header checksum only (20-B headers)
     if (cfg == 13) { L = 1500; mode = YU_MODE_IPV4; bytes = n * L; alg = 20 * n + 2 * n; }
+    // 14: uniform 1M x KB_LEN-byte UDP datagrams (default 72: 8-B header + 64-B payload)
+    if (cfg == 14) {
+      L = getenv("KB_LEN") ? (uint32_t)atoi(getenv("KB_LEN")) : 72u;
+      mode = YU_MODE_UDP;
+      bytes = n * L;
+      alg = bytes + 10 * n;
+    }
     if (cfg >= 4 && cfg <= 12) {
       // 4: BASELINE config 4 (U{64..9000}); 5: tun-like U{64..1500}; 6: U{40..200}
       // (RAW + initial); 7: U{64..1500} TCP segments, 8: U{40..200} UDP (TX kinds, addrs)

@@ -27,8 +27,8 @@ def short_name(full):
     k, args = m.group(1), [a.strip() for a in m.group(2).split(",")]
     if k == "k_small":
         return f"k_small<{args[0]},{args[1]}>"
-    if k == "k_tiny":
-        return f"k_tiny<{args[0]}>"
+    if k in ("k_tiny", "k_lane"):
+        return f"{k}<{args[0]}>"
     if k == "k_loop":
         return f"k_loop<{args[0]},{'BE' if args[2] == 'true' else 'LE'}>"
     if k == "k_seg":
@@ -59,7 +59,7 @@ def main(prof_dir, out_path):
     if os.path.exists(out_path):  # merge: configs not profiled in prof_dir keep their record
         with open(out_path) as f:
             res = json.load(f)
-    for c in "23467":
+    for c in "234678":
         cfg = f"config{c}"
         fpath = os.path.join(prof_dir, f"pmc_FETCH_SIZE_c{c}", "run_counter_collection.csv")
         wpath = os.path.join(prof_dir, f"pmc_WRITE_SIZE_c{c}", "run_counter_collection.csv")

@@ -48,6 +48,9 @@
 //   k_tiny<G>: uniform, packets <= 16G bytes, 4-aligned, no junk bytes: a wave
 //     step covers 64 packets, each load instruction one contiguous KiB, and a
 //     cross-lane transpose lets every lane finish one packet (BASELINE config 2).
+//   k_lane<U>: uniform, 4-aligned, 65..112 bytes (the 72-byte sendUDP
+//     datagram): 64 whole strides per wave step parked in LDS, one lane per
+//     packet summing it from there.
 //   k_small<G, U>: uniform stride, packet span <= G*U*16 bytes. A wave holds
 //     64/G packets per step; each group of G lanes loads its packet window in
 //     U dwordx4 loads per lane, reduces with log2(G) DPP adds and its last
@@ -55,7 +58,9 @@
 //   k_seg<U, NT, K>: ragged (tun-style, any alignment) batches and VERIFY_RX:
 //     a segmented sum over the byte stream of 64 consecutive packets per wave,
 //     U KiB tiles, packet sums as prefix differences (config 4, tun RX).
-//   k_rag<G, U>: ragged IPv4 header-only modes (<= 60 bytes of each packet).
+//   k_hdr<NT>: the IPv4 header-only modes (<= 60 bytes of each packet), uniform
+//     and ragged: one lane per packet, 32-byte reads.
+//   k_rag<G, U>: the first ragged kernel, kept as a measurement alternative.
 //   k_loop<U, BE>: one wave per packet, for uniform packets > 4 KiB.
 //   All are grid-stride kernels; the grid is sized per CU and over-subscribed
 //   (see blocks_per_cu), except that k_seg narrows it for small packets
@@ -592,6 +597,117 @@ __global__ __launch_bounds__(256) void k_tiny(BatchArgs A) {
       finish_packet(A, pf, le_to_be(mine, 0u), E, it.sd, A.fill ? A.fill + pf * A.stride : nullptr, E);
     if (!more) break;
     it = nx;
+    pb = pn;
+  }
+}
+
+// ---------------------------------------------------------------------
+// k_lane<U, NT>: uniform, 4-aligned packets of 65..16U bytes with
+// len <= stride <= 16U — the sizes where k_tiny<8> leaves lanes idle (a
+// 72-byte UDP datagram fills 5 of its 8 chunks) and k_small pays a group
+// reduction per packet. A wave step covers 64 packets, i.e. the contiguous
+// 64*stride bytes from packet pb on: U coalesced dwordx4 loads per lane,
+// parked in the wave's own LDS slice (no block barrier: LDS operations of one
+// wave complete in order). Each lane then sums its own packet from LDS, one
+// ds_read_b32 per dword, starting at dword lane % nd so that lanes whose
+// packets start on the same bank read different banks.
+// ---------------------------------------------------------------------
+template <int U>
+__device__ __forceinline__ void lane_fetch(const BatchArgs &A, const SidePtrs &sp,
+                                           uint64_t pb, uint32_t lane, uint32_t span,
+                                           bool nt, uint4 (&c)[U], Side &sd) {
+  const uint64_t base = uniform64((uint64_t)(uintptr_t)A.data + pb * A.stride);
+  const __amdgpu_buffer_rsrc_t r = rsrc_at(base, A.end);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t off = 16u * (64u * (uint32_t)u + lane);
+    c[u] = bld16(r, off < span ? off : kOOB, nt);
+  }
+  const uint64_t p = pb + lane;
+  sd = load_side(sp, p < A.n ? p : A.n - 1);
+}
+
+// LE sum of nw W-dword units of a lane's packet in LDS, starting at unit k0
+// and wrapping (summation order is free; the rotation spreads the lanes over
+// the LDS banks). W = 4 / 2 / 1: ds_read_b128 / b64 / b32.
+template <int W>
+__device__ __forceinline__ uint32_t lane_sum(const uint32_t *own, uint32_t nw, uint32_t k0) {
+  uint32_t acc = 0, k = k0;
+  for (uint32_t d = 0; d < nw; ++d) {
+    if (W == 4) {
+      const uint4 v = *(const uint4 *)(own + 4u * k);
+      acc = sad(v.w, sad(v.z, sad(v.y, sad(v.x, acc))));
+    } else if (W == 2) {
+      const uint2 v = *(const uint2 *)(own + 2u * k);
+      acc = sad(v.y, sad(v.x, acc));
+    } else {
+      acc = sad(own[k], acc);
+    }
+    k = k + 1u == nw ? 0u : k + 1u;
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int U, int NT>
+__global__ __launch_bounds__(256) void k_lane(BatchArgs A) {
+  __shared__ uint4 park[4][64 * U];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint4 *slice = park[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+  const uint64_t wave = grid_wave(A.xcd);
+  const uint64_t step = (uint64_t)gridDim.x * (blockDim.x >> 6) * 64u;
+  const SidePtrs sp = side_ptrs(A);
+  const uint32_t S = (uint32_t)A.stride;
+  const uint32_t E = A.len;
+  const uint32_t span = 64u * S;
+  const uint32_t nd = (E + 3u) >> 2;  // dwords per packet
+  // bytes past E in the last dword (the dword-granular sum takes them)
+  const uint32_t junk_tail = (E & 3u) ? ~((1u << (8u * (E & 3u))) - 1u) : 0u;
+  // TX modes: Encode leaves the 16-bit checksum field 0; starts are 4-aligned
+  // and the field offset even, so it is half of dword f/4
+  const uint32_t f = mode_field(A.mode);
+  const bool tx = mode_is_tx(A.mode);
+  const uint32_t junk_field = 0xFFFFu << (8u * (f & 3u));
+  // widest LDS read that tiles the packet and stays aligned (wave-uniform)
+  const uint32_t W = ((E | S) & 15u) == 0 ? 4u : (((E | S) & 7u) == 0 ? 2u : 1u);
+  const uint32_t nw = nd / W;
+  const uint32_t k0 = lane % nw;
+  const uint32_t *own = (const uint32_t *)slice + lane * (S >> 2);
+
+  uint64_t pb = wave * 64u;
+  if (pb >= A.n) return;
+  uint4 c[U];
+  Side sd;
+  lane_fetch<U>(A, sp, pb, lane, span, NT != 0, c, sd);
+  for (;;) {
+    const uint64_t pn = pb + step;
+    const bool more = pn < A.n;  // wave-uniform
+    uint4 nx[U];
+    Side nsd;
+    lane_fetch<U>(A, sp, more ? pn : A.n, lane, span, NT != 0, nx, nsd);
+
+#pragma unroll
+    for (int u = 0; u < U; ++u) slice[64 * u + lane] = c[u];
+    wave_lds_fence();
+    uint32_t acc = W == 4u ? lane_sum<4>(own, nw, k0)
+                           : (W == 2u ? lane_sum<2>(own, nw, k0) : lane_sum<1>(own, nw, k0));
+    // the sum is exact (<= 128 bytes), so junk bytes come off by subtraction
+    if (junk_tail) acc -= sad(own[nd - 1u] & junk_tail, 0u);
+    if (tx) acc -= sad(own[f >> 2] & junk_field, 0u);
+    wave_lds_fence();  // the next step's stores stay behind these reads
+
+    const uint64_t p = pb + lane;
+    if (p < A.n)
+      finish_packet(A, p, le_to_be(acc, 0u), E, sd, A.fill ? A.fill + p * A.stride : nullptr, E);
+    if (!more) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = nx[u];
+    sd = nsd;
     pb = pn;
   }
 }
@@ -1456,6 +1572,11 @@ struct Variant {
 
 const Variant kTiny[] = {YU_TINY(4), YU_TINY(8)};
 
+// window = the largest stride a wave step's U KiB hold (64 packets)
+#define YU_LANE(U) \
+  {"k_lane<" #U ">", 16u * U, {k_lane<U, 0>, k_lane<U, 1>, k_lane<U, 1>}, 1, 64u}
+const Variant kLane[] = {YU_LANE(5), YU_LANE(6), YU_LANE(7), YU_LANE(8)};
+
 // Ordered by window; for each window the variant with the most packets per
 // wave comes first (amortises the per-packet epilogue over more bytes).
 const Variant kSmall[] = {
@@ -1519,6 +1640,10 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
   };
   // k_tiny: no junk bytes (4-aligned starts, no TX field, no IPv4 header walk)
   const bool tiny_ok = aligned4 && !mode_is_ipv4(mode) && mode != YU_MODE_VERIFY_RX;
+  // k_lane: the same modes, one wave step = 64 whole strides in LDS
+  auto lane_fits = [&](const Variant &v) {
+    return tiny_ok && (stride & 3u) == 0 && len <= stride && stride <= v.window;
+  };
   if (mode == YU_MODE_VERIFY_RX) return pick_ragged(mode);
   // IPv4 header-only modes: one lane per packet (1M x 1500-B datagrams:
   // 29.9 us vs 36.9 with k_small<4,1>, kbench 13)
@@ -1530,7 +1655,16 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
       if (strcmp(v.name, f) == 0 && fits(v)) return v;
     for (const Variant &v : kTiny)
       if (strcmp(v.name, f) == 0 && tiny_ok && fits(v)) return v;
+    for (const Variant &v : kLane)
+      if (strcmp(v.name, f) == 0 && lane_fits(v)) return v;
   }
+  // k_tiny<4> up to 64 bytes, k_lane to 112 (72-byte UDP datagrams: 16.4 vs
+  // 20.0 us with k_tiny<8>, 96 bytes: 19.3 vs 21.0), k_tiny<8> above, where
+  // all its lanes load (128 bytes: 23.6 vs 24.6 us; tools/kbench 14)
+  if (tiny_ok && len <= 64u && fits(kTiny[0])) return kTiny[0];
+  if (len <= 112u)
+    for (const Variant &v : kLane)
+      if (lane_fits(v)) return v;
   if (tiny_ok)
     for (const Variant &v : kTiny)
       if (fits(v)) return v;
