@@ -303,7 +303,7 @@ int wait_flag(Slot &x, uint32_t seq) {
 
 template <class Layout>
 int direct(Slot &x, const Layout &L, uint64_t n, const uint16_t *h_init,
-           const uint8_t *h_addrs, uint16_t *h_out, bool pin_out) {
+           const uint8_t *h_addrs, uint16_t *h_out) {
   const uint8_t *src = L.stage(x, 0, n);  // the caller's pinned bytes or the slot's staging
   uint8_t *d = nullptr, *da = nullptr;
   uint64_t *doff = nullptr;
@@ -332,7 +332,6 @@ int direct(Slot &x, const Layout &L, uint64_t n, const uint16_t *h_init,
   rc = wait_flag(x, seq);
   if (rc) return rc;
   memcpy(h_out, x.h_outc, n * 2);
-  (void)pin_out;
   return YU_OK;
 }
 
@@ -354,11 +353,11 @@ int pipeline(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
   }
   int rc = c.reserve(max_b, max_pk);
   if (rc) return rc;
-  const bool pin_out = is_pinned(h_out);
   if (max_pk == n && max_b <= direct_max()) {
-    rc = direct(c.s[0], L, n, h_init, h_addrs, h_out, pin_out);
+    rc = direct(c.s[0], L, n, h_init, h_addrs, h_out);
     if (rc != kNoDirect) return rc;
   }
+  const bool pin_out = is_pinned(h_out);
   uint64_t k = 0;
   for (uint64_t first = 0; first < n; ++k) {
     Slot &x = c.s[k % kSlots];
