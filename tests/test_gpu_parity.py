@@ -715,3 +715,89 @@ def test_fill_ragged_ipv4_headers(dev, oracle_c):
     assert np.array_equal(fields, want)
     v = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), "verify_ipv4")
     assert bool(batch.verified(v).all())
+
+
+_MIN_LEN = {O.MODE_UDP: 8, O.MODE_TCP: 20, O.MODE_VERIFY_TCP: 20, O.MODE_ICMP: 4,
+            O.MODE_IPV4: 1, O.MODE_VERIFY_IPV4: 1}
+_FIELD = {O.MODE_UDP: 6, O.MODE_TCP: 16, O.MODE_ICMP: 2}
+
+
+def _fuzz_lens(rng, n, lo):
+    kind = int(rng.integers(0, 4))
+    if kind == 0:   # tiny
+        hi = 80
+    elif kind == 1:  # tun-like
+        hi = 1600
+    elif kind == 2:  # mixed with jumbo
+        hi = 9100
+    else:            # one size
+        return np.full(n, int(rng.integers(lo, 2000)), np.int64)
+    return rng.integers(lo, max(lo, hi) + 1, size=n)
+
+
+def _fuzz_headers(rng, blob, starts, lens, mode):
+    for s, ln in zip(starts, lens):
+        s, ln = int(s), int(ln)
+        if mode in (O.MODE_TCP, O.MODE_VERIFY_TCP):
+            blob[s + 12] = (4 * int(rng.integers(5, min(60, ln) // 4 + 1)) // 4) << 4
+        if mode in (O.MODE_IPV4, O.MODE_VERIFY_IPV4):
+            ihl = int(rng.integers(0, 16))
+            blob[s] = 0x40 | (ihl if ihl * 4 <= ln else ln // 4 & 0xF)
+
+
+def test_random_batches_fuzz(dev, oracle_c):
+    """Randomised geometry x mode x side data x fill: every kernel variant the
+    selection can pick (k_tiny, k_lane, k_small, k_hdr, k_seg, k_loop), against the
+    C oracle on the same bytes. Seeded, so a failure reproduces."""
+    rng = np.random.default_rng(2026)
+    seen = set()
+    for it in range(800):
+        mode = int(rng.integers(0, 8))  # VERIFY_RX has its own tests (real headers)
+        lo = _MIN_LEN.get(mode, 0)
+        n = int(rng.choice([1, 2, 63, 64, 65, int(rng.integers(1, 3000))]))
+        ragged = bool(rng.integers(0, 2))
+        side = int(rng.integers(0, 3))  # 0: scalar initial, 1: initial_arr, 2: addrs
+        tx = mode in _FIELD or mode == O.MODE_IPV4
+        fill = tx and bool(rng.integers(0, 2))
+        init = rng.integers(0, 65536, size=n, dtype=np.uint16) if side == 1 else None
+        addrs = _rand(rng, 8 * n) if side == 2 else None
+        initial = int(rng.integers(0, 65536)) if side == 0 else 0
+        if ragged:
+            lens = _fuzz_lens(rng, n, lo)
+            base = int(rng.integers(0, 16))
+            offs = np.zeros(n + 1, np.uint64)
+            offs[1:] = np.cumsum(lens)
+            offs += base
+            blob = _rand(rng, int(offs[-1]) + 16, ["rand", "rand", "rand", "zero", "ff"][it % 5])
+            _fuzz_headers(rng, blob, offs[:-1], lens, mode)
+            want = oracle_c.batch(blob, mode, offsets=offs, initial_arr=init, initial=initial, addrs=addrs)
+            d = _to(dev, blob)
+            seen.add(batch.ragged_variant(mode))
+            got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), mode, initial=initial,
+                                        initial_arr=None if init is None else _to(dev, init),
+                                        addrs=None if addrs is None else _to(dev, addrs),
+                                        fill=fill).cpu().numpy()
+            starts = offs[:-1].astype(np.int64)
+        else:
+            length = int(_fuzz_lens(rng, 1, lo)[0])
+            align = 0 if fill else int(rng.integers(0, 4))
+            pad = int(rng.integers(0, 3)) * (4 if fill else int(rng.integers(1, 6)))
+            stride = (length + 3) // 4 * 4 + pad if fill else length + pad
+            blob = _rand(rng, align + (n - 1) * stride + length + 16, ["rand", "zero", "ff"][it % 3])
+            starts = align + stride * np.arange(n, dtype=np.int64)
+            _fuzz_headers(rng, blob, starts, np.full(n, length), mode)
+            want = oracle_c.batch(blob[align:], mode, stride=stride, length=length, n=n,
+                                  initial_arr=init, initial=initial, addrs=addrs)
+            d = _to(dev, blob)
+            seen.add(batch.variant(stride, length, mode, align))
+            got = batch.checksum_uniform(d[align:], stride, length, n, mode, initial=initial,
+                                         initial_arr=None if init is None else _to(dev, init),
+                                         addrs=None if addrs is None else _to(dev, addrs),
+                                         fill=fill).cpu().numpy()
+        assert np.array_equal(got, want), (it, mode, ragged, n, side, fill, np.nonzero(got != want)[0][:8])
+        if fill and mode in _FIELD:
+            f = _FIELD[mode]
+            h = d.cpu().numpy()
+            fields = (h[starts + f].astype(np.uint16) << 8) | h[starts + f + 1]
+            assert np.array_equal(fields, want), (it, mode, ragged)
+    assert {"k_tiny<4>", "k_small<16,6>", "k_hdr"} <= seen or len(seen) >= 6, seen
