@@ -116,14 +116,23 @@ int main(int argc, char **argv) {
       if (cfg == 13) set_ihl_stride<<<1024, 256>>>(bufs[r], L, n);
     }
     CK(hipDeviceSynchronize());
+    // KB_FILL=1: the in-place field writer (TX modes) with no uint16 output
+    const bool fill = getenv("KB_FILL") && atoi(getenv("KB_FILL"));
     auto launch = [&](int k) {
       const bool ph = mode == YU_MODE_UDP || mode == YU_MODE_TCP || mode == YU_MODE_VERIFY_TCP ||
                       mode == YU_MODE_VERIFY_UDP;
       const uint16_t *ia = mode == YU_MODE_RAW ? init : nullptr;
-      int rc = d_off ? yu_csum_batch_ragged(bufs[k % R], d_off, n, mode, ia, 0, ph ? addrs : nullptr,
-                                            out, nullptr)
-                     : yu_csum_batch_uniform(bufs[k % R], L, L, n, mode, ia, 0, ph ? addrs : nullptr, out,
-                                             nullptr);
+      int rc;
+      if (fill)
+        rc = d_off ? yu_csum_fill_ragged(bufs[k % R], d_off, n, mode, ia, 0, ph ? addrs : nullptr,
+                                         nullptr, nullptr)
+                   : yu_csum_fill_uniform(bufs[k % R], L, L, n, mode, ia, 0, ph ? addrs : nullptr,
+                                          nullptr, nullptr);
+      else
+        rc = d_off ? yu_csum_batch_ragged(bufs[k % R], d_off, n, mode, ia, 0, ph ? addrs : nullptr,
+                                          out, nullptr)
+                   : yu_csum_batch_uniform(bufs[k % R], L, L, n, mode, ia, 0, ph ? addrs : nullptr, out,
+                                           nullptr);
       if (rc) { fprintf(stderr, "rc %d\n", rc); exit(1); }
     };
     for (int r = 0; r < rounds; ++r) {
