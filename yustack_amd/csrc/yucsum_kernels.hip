@@ -568,7 +568,47 @@ __device__ __forceinline__ uint32_t bcast_last(uint32_t v, uint32_t lane) {
   return (uint32_t)__shfl(v, (int)(lane | (G - 1)), 64);
 }
 
-template <int G, int NT>
+// Fill with whole chunks (k_tiny): lane (g, f/16) of slot k holds the field
+// chunk of packet pb + (64/G)k + g, whose value lane (g, k) computed. It patches
+// the field in its register copy, and every slot goes back out with the same
+// offsets it was loaded from. Only when no chunk reaches into the next packet
+// (stride >= the 16-byte-rounded length), and never past the batch's last whole
+// dword (the last packet's partial tail dword holds no field).
+template <int G>
+__device__ __forceinline__ void tiny_store(const BatchArgs &A, uint64_t pb, uint32_t g, uint32_t j,
+                                           const TinyItem<G> &it, uint32_t be, uint32_t f) {
+  constexpr uint32_t GPW = 64 / G;
+  const uint64_t e4 = A.end & ~3ull;  // packets start 4-aligned (fill contract)
+  const uint32_t fd = (f >> 2) & 3u, sh = (f & 2u) * 8u;
+  const uint32_t m = 0xFFFFu << sh;
+  const bool holder = j == (f >> 4);
+  const bool in = 16u * j < A.len;
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    const uint32_t v = ((uint32_t)__shfl((int)be, (int)(g * G + (uint32_t)k), 64)) << sh;
+    uint4 c = it.c[k];
+    if (holder) {
+      c.x = fd == 0 ? (c.x & ~m) | v : c.x;
+      c.y = fd == 1 ? (c.y & ~m) | v : c.y;
+      c.z = fd == 2 ? (c.z & ~m) | v : c.z;
+      c.w = fd == 3 ? (c.w & ~m) | v : c.w;
+    }
+    const uint64_t q = pb + GPW * (uint32_t)k + g;
+    uint32_t *dst = (uint32_t *)(A.fill + q * A.stride + 16u * j);
+    const uint64_t da = (uint64_t)(uintptr_t)dst;
+    if (in && q < A.n) {
+      if (da + 16u <= e4) {
+        *(uint4 *)dst = c;
+      } else {  // the batch's last chunk: whole dwords only
+        if (da + 4u <= e4) dst[0] = c.x;
+        if (da + 8u <= e4) dst[1] = c.y;
+        if (da + 12u <= e4) dst[2] = c.z;
+      }
+    }
+  }
+}
+
+template <int G, int NT, bool WB = false>
 __global__ __launch_bounds__(256) void k_tiny(BatchArgs A) {
   constexpr uint32_t GPW = 64 / G;
   const uint32_t lane = threadIdx.x & 63u;
@@ -590,6 +630,9 @@ __global__ __launch_bounds__(256) void k_tiny(BatchArgs A) {
   const uint32_t fd = (f >> 2) & 3u;
   const uint4 m4 = make_uint4(fd == 0 ? fm : ~0u, fd == 1 ? fm : ~0u, fd == 2 ? fm : ~0u,
                               fd == 3 ? fm : ~0u);
+  // fill with whole chunks (tiny_store): its own instantiation, so the plain
+  // kernel keeps its registers
+  const bool wb = WB && A.fill && A.stride >= ((A.len + 15u) & ~15u);
 
   uint64_t pb = wave * 64u;
   if (pb >= A.n) return;
@@ -612,8 +655,13 @@ __global__ __launch_bounds__(256) void k_tiny(BatchArgs A) {
       mine = (j == (uint32_t)k) ? acc : mine;
     }
     const uint64_t pf = pb + GPW * j + g;
-    if (pf < A.n)
+    if (wb) {
+      const uint32_t r = packet_value(A, le_to_be(mine, 0u), E, it.sd);
+      if (pf < A.n && A.out) A.out[pf] = (uint16_t)r;
+      tiny_store<G>(A, pb, g, j, it, ((r >> 8) | (r << 8)) & 0xFFFFu, f);
+    } else if (pf < A.n) {
       finish_packet(A, pf, le_to_be(mine, 0u), E, it.sd, A.fill ? A.fill + pf * A.stride : nullptr, E);
+    }
     if (!more) break;
     it = nx;
     pb = pn;
@@ -1612,14 +1660,17 @@ struct Variant {
   KernelFn fn[3];   // by load policy (bld16): plain, nt, hybrid
   uint32_t G;       // lanes per packet
   uint32_t ppw;     // packets per wave step
+  KernelFn fill = nullptr;  // in-place fill instantiation, if it has its own
 };
 
 #define YU_SMALL(G, U) \
   {"k_small<" #G "," #U ">", 16u * G * U, {k_small<G, U, 0>, k_small<G, U, 1>, k_small<G, U, 2>}, G, 64u / G}
-#define YU_TINY(G) \
-  {"k_tiny<" #G ">", 16u * G, {k_tiny<G, 0>, k_tiny<G, 1>, k_tiny<G, 1>}, G, 64u}
+#define YU_TINY(G, FILL) \
+  {"k_tiny<" #G ">", 16u * G, {k_tiny<G, 0>, k_tiny<G, 1>, k_tiny<G, 1>}, G, 64u, FILL}
 
-const Variant kTiny[] = {YU_TINY(4), YU_TINY(8)};
+// k_tiny<8> (113..128 bytes) fills with single field stores: its whole-chunk
+// instantiation would spill scalar registers
+const Variant kTiny[] = {YU_TINY(4, (k_tiny<4, 1, true>)), YU_TINY(8, nullptr)};
 
 // window = the largest stride a wave step's U KiB hold (64 packets)
 #define YU_LANE(U) \
@@ -1800,7 +1851,8 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   BatchArgs a = A;
   a.xcd = (uint32_t)use_xcd();
   a.small_waves = (uint32_t)cu_count(dev) * 4u * (uint32_t)seg_small_blocks();
-  hipLaunchKernelGGL(v.fn[use_nt()], dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  const KernelFn k = A.fill && v.fill ? v.fill : v.fn[use_nt()];
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
 
