@@ -192,18 +192,52 @@ func BatchHostRagged(data []byte, offsets []uint64, mode Mode, initial []uint16,
 
 // BatchHostPackets computes one result per packet of a burst given as one
 // slice per packet (buffer.View, buffer/view.go:4), gathered by the library
-// into its pinned staging. The views' Go memory is pinned (runtime.Pinner)
-// for the call, because the C-allocated iovec array holds pointers into it;
-// the library keeps none of them after returning.
+// into its pinned staging (see withPackets).
 func BatchHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, out []uint16,
 	devices ...int) error {
-	n := len(pkts)
-	if n == 0 {
+	if len(pkts) == 0 {
 		return nil
 	}
-	if len(out) < n {
+	if len(out) < len(pkts) {
 		return fmt.Errorf("checksum: batch buffers too small")
 	}
+	pi, pa := sideArgs(initial, addrs)
+	d, nd := deviceList(devices)
+	return withPackets(pkts, func(iov *C.yu_iovec, first *C.uint64_t, n C.uint64_t) C.int {
+		return C.yu_csum_batch_host_iov_multi(iov, first, n, C.int(mode), pi, 0, pa,
+			(*C.uint16_t)(unsafe.Pointer(&out[0])), &d[0], C.int(nd))
+	})
+}
+
+// FillHostPackets is the batched TX step of sendUDP / sendTCP / WritePacket /
+// sendICMPv4: for each outgoing packet (one slice, as Encode left it, field 0)
+// it computes the checksum and stores it big-endian into the packet's field
+// in place, like SetChecksum (header/udp.go:60-62, header/tcp.go:156-158,
+// header/ipv4.go:165-167, header/icmpv4.go:46-48). mode is ModeUDP, ModeTCP,
+// ModeIPv4 or ModeICMP; out (len n) may be nil.
+func FillHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, out []uint16,
+	device int) error {
+	if len(pkts) == 0 {
+		return nil
+	}
+	var po *C.uint16_t
+	if out != nil {
+		if len(out) < len(pkts) {
+			return fmt.Errorf("checksum: batch buffers too small")
+		}
+		po = (*C.uint16_t)(unsafe.Pointer(&out[0]))
+	}
+	pi, pa := sideArgs(initial, addrs)
+	return withPackets(pkts, func(iov *C.yu_iovec, first *C.uint64_t, n C.uint64_t) C.int {
+		return C.yu_csum_fill_host_iov(iov, first, n, C.int(mode), pi, 0, pa, po, C.int(device))
+	})
+}
+
+// withPackets passes one view per packet to call as a C iovec array. The
+// views' Go memory is pinned (runtime.Pinner) for the call, because the
+// C-allocated array holds pointers into it; the library keeps none of them.
+func withPackets(pkts [][]byte, call func(*C.yu_iovec, *C.uint64_t, C.uint64_t) C.int) error {
+	n := len(pkts)
 	var pin runtime.Pinner
 	defer pin.Unpin()
 	iov := unsafe.Slice((*C.yu_iovec)(C.malloc(C.size_t(n)*C.size_t(unsafe.Sizeof(C.yu_iovec{})))), n)
@@ -219,8 +253,5 @@ func BatchHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, 
 		iov[i].len = C.uint64_t(len(p))
 		first[i+1] = uint64(i + 1)
 	}
-	pi, pa := sideArgs(initial, addrs)
-	d, nd := deviceList(devices)
-	return status(C.yu_csum_batch_host_iov_multi(&iov[0], (*C.uint64_t)(unsafe.Pointer(&first[0])),
-		C.uint64_t(n), C.int(mode), pi, 0, pa, (*C.uint16_t)(unsafe.Pointer(&out[0])), &d[0], C.int(nd)))
+	return status(call(&iov[0], (*C.uint64_t)(unsafe.Pointer(&first[0])), C.uint64_t(n)))
 }

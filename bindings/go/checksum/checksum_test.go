@@ -90,3 +90,33 @@ func TestBatchHostPackets(t *testing.T) {
 		}
 	}
 }
+
+// FillHostPackets sets each ICMP echo's checksum field in place: afterwards every
+// packet sums to 0xFFFF, as checker-style verification expects, and the value
+// stored is the complement of the sum with the field zero (sendICMPv4,
+// network/ipv4/icmp.go:36-45).
+func TestFillHostPackets(t *testing.T) {
+	pkts := make([][]byte, 500)
+	want := make([]uint16, len(pkts))
+	for i := range pkts {
+		pkts[i] = make([]byte, 8+(i*29)%1400)
+		for j := range pkts[i] {
+			pkts[i][j] = byte(i*17 + j*3)
+		}
+		pkts[i][2], pkts[i][3] = 0, 0
+		want[i] = ^Checksum(pkts[i], 0)
+	}
+	if err := FillHostPackets(pkts, ModeICMP, nil, nil, nil, 0); err == ErrNoDevice {
+		t.Skip("no HIP device")
+	} else if err != nil {
+		t.Fatal(err)
+	}
+	for i, p := range pkts {
+		if got := uint16(p[2])<<8 | uint16(p[3]); got != want[i] {
+			t.Fatalf("packet %d: field %#x want %#x", i, got, want[i])
+		}
+		if s := Checksum(p, 0); s != 0xffff {
+			t.Fatalf("packet %d: sums to %#x after fill", i, s)
+		}
+	}
+}

@@ -245,6 +245,26 @@ int yu_csum_batch_host_iov(const yu_iovec *iov, const uint64_t *first_iov,
                            uint16_t initial, const uint8_t *h_addrs,
                            uint16_t *h_out, int device);
 
+/* Host-memory field writer: the matching yu_csum_batch_host_* call (TX modes
+ * UDP/TCP/IPV4/ICMP only), then each result stored big-endian into the
+ * packet's checksum field in host memory, as the device writer does
+ * (yu_csum_fill_uniform). `h_out` may be NULL. The iov form writes through
+ * the views (their `base` must be writable memory). Synchronous. */
+int yu_csum_fill_host_uniform(uint8_t *h_data, uint64_t stride, uint32_t len,
+                              uint64_t n, int mode,
+                              const uint16_t *h_initial_arr, uint16_t initial,
+                              const uint8_t *h_addrs, uint16_t *h_out,
+                              int device);
+int yu_csum_fill_host_ragged(uint8_t *h_data, const uint64_t *h_offsets,
+                             uint64_t n, int mode,
+                             const uint16_t *h_initial_arr, uint16_t initial,
+                             const uint8_t *h_addrs, uint16_t *h_out,
+                             int device);
+int yu_csum_fill_host_iov(const yu_iovec *iov, const uint64_t *first_iov,
+                          uint64_t n, int mode, const uint16_t *h_initial_arr,
+                          uint16_t initial, const uint8_t *h_addrs,
+                          uint16_t *h_out, int device);
+
 /* Multi-GPU host path (SURVEY.md §8b `yu_csum_batch_host(..., ngpu)`, §8e):
  * the same three calls with the batch split into ndev contiguous shards, one
  * per entry of `devices` (a device may be listed more than once), each shard

@@ -297,6 +297,29 @@ inline void HostPackets(const yu_iovec *iov, const uint64_t *first_iov, uint64_t
   if (rc) throw Error(rc, "yu_csum_batch_host_iov_multi");
 }
 
+// Host-memory field writer (SetChecksum in place, TX modes): the batch above,
+// then each result stored big-endian into the packet's field. `out` may be null.
+inline void FillHostUniform(uint8_t *data, uint64_t stride, uint32_t len, uint64_t n, Mode m,
+                            uint16_t *out = nullptr, const Side &s = {}, int device = 0) {
+  int rc = yu_csum_fill_host_uniform(data, stride, len, n, m, s.initial_arr, s.initial, s.addrs,
+                                     out, device);
+  if (rc) throw Error(rc, "yu_csum_fill_host_uniform");
+}
+
+inline void FillHostRagged(uint8_t *data, const uint64_t *offsets, uint64_t n, Mode m,
+                           uint16_t *out = nullptr, const Side &s = {}, int device = 0) {
+  int rc = yu_csum_fill_host_ragged(data, offsets, n, m, s.initial_arr, s.initial, s.addrs, out,
+                                    device);
+  if (rc) throw Error(rc, "yu_csum_fill_host_ragged");
+}
+
+inline void FillHostPackets(const yu_iovec *iov, const uint64_t *first_iov, uint64_t n, Mode m,
+                            uint16_t *out = nullptr, const Side &s = {}, int device = 0) {
+  int rc = yu_csum_fill_host_iov(iov, first_iov, n, m, s.initial_arr, s.initial, s.addrs, out,
+                                 device);
+  if (rc) throw Error(rc, "yu_csum_fill_host_iov");
+}
+
 }  // namespace batch
 }  // namespace yustack
 

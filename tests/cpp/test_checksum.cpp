@@ -234,6 +234,13 @@ static void test_gpu_batches() {
   for (uint64_t i = 0; i < n; ++i)
     EXPECT(hout[i] == checksum::Checksum(segs.data() + i, 20, 0), "host multi raw %lu", i);
 
+  // host field writer: the harness's segments with their fields zeroed (as
+  // Encode leaves them) come back byte-identical to the originals
+  std::vector<uint8_t> blank(segs);
+  for (uint64_t i = 0; i < n; ++i) blank[soff[i] + 16] = blank[soff[i] + 17] = 0;
+  batch::FillHostRagged(blank.data(), soff.data(), n, batch::TCP, nullptr, hside);
+  EXPECT(blank == segs, "host fill restores every TCP checksum field");
+
   bool threw = false;
   try {
     batch::Uniform(d_segs, 16, 70000, 1, batch::TCP, d_out);

@@ -103,6 +103,10 @@ def test_argument_validation_precedes_device():
     assert L.yu_csum_fill_uniform(p + 1, 16, 16, 4, 1, None, 0, None, o, None) == _lib.YU_EINVAL  # unaligned
     assert L.yu_csum_batch_ragged(p, None, 4, 0, None, 0, None, o, None) == _lib.YU_EINVAL
     assert L.yu_csum_batch_host_uniform(p, 16, 16, 4, 99, None, 0, None, o, 0) == _lib.YU_EINVAL
+    for f in (L.yu_csum_fill_host_ragged, L.yu_csum_fill_host_iov):  # RAW / verify: not TX
+        assert f(p, p, 4, 0, None, 0, None, o, 0) == _lib.YU_EINVAL
+        assert f(p, p, 4, 6, None, 0, None, o, 0) == _lib.YU_EINVAL
+    assert L.yu_csum_fill_host_uniform(p, 16, 16, 4, 0, None, 0, None, o, 0) == _lib.YU_EINVAL
     # host ragged / iov: offsets and views are host memory, checked before any device work
     bad = (ctypes.c_uint64 * 5)(0, 16, 8, 48, 64)  # decreasing
     assert L.yu_csum_batch_host_ragged(p, ctypes.addressof(bad), 4, 0, None, 0, None, o, 0) == _lib.YU_EINVAL

@@ -806,3 +806,69 @@ def test_random_batches_fuzz(dev, oracle_c):
                 fields = (h[starts + f].astype(np.uint16) << 8) | h[starts + f + 1]
                 assert np.array_equal(fields, want), (it, mode, ragged)
     assert {"k_tiny<4>", "k_small<16,6>", "k_hdr"} <= seen or len(seen) >= 6, seen
+
+
+def test_host_fill_paths(dev, oracle_c):
+    """Host-memory field writer (yu_csum_fill_host_*): each TX field is set to the
+    oracle's value in the caller's buffer, nothing else changes, and the filled
+    packets verify. Covers the direct (small) and pipelined (large) host paths,
+    views that split the field, and IPv4 headers whose IHL leaves no room."""
+    rng = np.random.default_rng(909)
+    fld = {O.MODE_UDP: 6, O.MODE_TCP: 16, O.MODE_ICMP: 2, O.MODE_IPV4: 10}
+
+    def check(before, after, starts, want, mode, may_skip=None):
+        f = fld[mode]
+        may = np.zeros(len(before), bool)
+        may[starts + f] = True
+        may[starts + f + 1] = True
+        assert np.array_equal(after[~may], before[~may])
+        got = (after[starts + f].astype(np.uint16) << 8) | after[starts + f + 1]
+        keep = np.ones(len(starts), bool) if may_skip is None else ~may_skip
+        assert np.array_equal(got[keep], want[keep])
+        if may_skip is not None:  # no room for the field: left as it was
+            assert np.array_equal(after[starts[may_skip] + f], before[starts[may_skip] + f])
+
+    for n, L in ((300, 1500), (40_000, 1500), (5000, 72)):  # direct, pipelined, small
+        for mode in (O.MODE_UDP, O.MODE_TCP, O.MODE_ICMP):
+            host = _rand(rng, n * L)
+            if mode == O.MODE_TCP:
+                host[12::L] = 0x50
+            addrs = _rand(rng, 8 * n)
+            want = oracle_c.batch(host, mode, stride=L, length=L, n=n,
+                                  addrs=addrs if mode in (1, 2) else None)
+            buf = host.copy()
+            out = batch.checksum_host_uniform(buf, L, L, n, mode, addrs=addrs if mode in (1, 2) else None,
+                                              fill=True)
+            assert np.array_equal(out, want)
+            check(host, buf, L * np.arange(n), want, mode)
+    # ragged IPv4 headers, some with IHL < 3 (field outside the header: not written)
+    n = 2000
+    lens = rng.integers(20, 1501, size=n)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    blob = _rand(rng, int(offs[-1]))
+    starts = offs[:-1].astype(np.int64)
+    ihl = rng.integers(0, 16, size=n)
+    blob[starts] = (0x40 | ihl).astype(np.uint8)
+    want = oracle_c.batch(blob, O.MODE_IPV4, offsets=offs)
+    buf = blob.copy()
+    out = batch.checksum_host_ragged(buf, offs, "ipv4", fill=True)
+    assert np.array_equal(out, want)
+    check(blob, buf, starts, want, O.MODE_IPV4, may_skip=np.minimum(ihl * 4, lens) < 12)
+    v = batch.checksum_host_ragged(buf, offs, "verify_ipv4")
+    assert np.isin(v[np.minimum(ihl * 4, lens) >= 12], (0, 0xFFFF)).all()
+    # scatter-gather UDP datagrams split inside the 8-byte header (the field straddles)
+    n = 500
+    pk = [_rand(rng, int(rng.integers(8, 300))) for _ in range(n)]
+    addrs = _rand(rng, 8 * n)
+    flat = np.concatenate(pk)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in pk])
+    want = oracle_c.batch(flat, O.MODE_UDP, offsets=offs, addrs=addrs)
+    views = [[p[:7], p[7:]] for p in [p.copy() for p in pk]]
+    out = batch.checksum_host_iov(views, "udp", addrs=addrs, fill=True)
+    assert np.array_equal(out, want)
+    after = np.concatenate([np.concatenate(v) for v in views])
+    check(flat, after, offs[:-1].astype(np.int64), want, O.MODE_UDP)
+    with pytest.raises(TypeError):
+        batch.checksum_host_iov([[bytes(8)]], "udp", fill=True)

@@ -20,6 +20,7 @@ EXPORTS = (
     "yu_csum_batch_host_uniform", "yu_csum_batch_host_ragged", "yu_csum_batch_host_iov",
     "yu_csum_batch_host_uniform_multi", "yu_csum_batch_host_ragged_multi",
     "yu_csum_batch_host_iov_multi",
+    "yu_csum_fill_host_uniform", "yu_csum_fill_host_ragged", "yu_csum_fill_host_iov",
     "yu_abi_version", "yu_strerror", "yu_device_count", "yu_uniform_variant",
     "yu_ragged_variant",
 )
@@ -73,6 +74,12 @@ def lib() -> ctypes.CDLL:
     L.yu_csum_batch_host_ragged.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, i32]
     L.yu_csum_batch_host_iov.restype = i32
     L.yu_csum_batch_host_iov.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, i32]
+    L.yu_csum_fill_host_uniform.restype = i32
+    L.yu_csum_fill_host_uniform.argtypes = [vp, u64, u32, u64, i32, vp, u16, vp, vp, i32]
+    L.yu_csum_fill_host_ragged.restype = i32
+    L.yu_csum_fill_host_ragged.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, i32]
+    L.yu_csum_fill_host_iov.restype = i32
+    L.yu_csum_fill_host_iov.argtypes = [vp, vp, u64, i32, vp, u16, vp, vp, i32]
     L.yu_csum_batch_host_uniform_multi.restype = i32
     L.yu_csum_batch_host_uniform_multi.argtypes = [vp, u64, u32, u64, i32, vp, u16, vp, vp, vp, i32]
     L.yu_csum_batch_host_ragged_multi.restype = i32

@@ -145,22 +145,42 @@ def checksum_ragged(data: torch.Tensor, offsets: torch.Tensor, mode="raw", *, in
     return out
 
 
-def checksum_host_uniform(data: np.ndarray, stride: int, length: int, n: int, mode="raw", *,
-                          initial: int = 0, initial_arr: np.ndarray | None = None,
-                          addrs: np.ndarray | None = None, out: np.ndarray | None = None,
-                          device: int | list[int] = 0) -> np.ndarray:
-    """Host-memory batch in, host-memory results out (pinned staging + pipelined
-    H2D/kernel/D2H inside the library). ``data`` may be a numpy array or a pinned
-    torch CPU tensor (then the copy engine reads it directly). ``device`` may be a
-    list of device indices: one shard per GPU, all at once."""
-    m = _mode(mode)
+def _host_data(data, fill: bool):
+    """Pointer and size of a host byte buffer; with ``fill`` the fields are written
+    into it, so it must be the caller's own writable contiguous uint8 memory."""
     if isinstance(data, torch.Tensor):
         if data.is_cuda or data.dtype != torch.uint8 or not data.is_contiguous():
             raise TypeError("data must be a contiguous uint8 CPU tensor")
-        dptr, dlen = data.data_ptr(), data.numel()
+        return data, data.data_ptr(), data.numel()
+    if fill:
+        if not (isinstance(data, np.ndarray) and data.dtype == np.uint8 and data.flags.c_contiguous
+                and data.flags.writeable):
+            raise TypeError("fill=True needs a writable C-contiguous uint8 numpy array")
     else:
         data = np.ascontiguousarray(data, dtype=np.uint8)
-        dptr, dlen = data.ctypes.data, data.size
+    return data, data.ctypes.data, data.size
+
+
+def _fill_name(name: str, fill: bool, device) -> str:
+    if not fill:
+        return name
+    if isinstance(device, (list, tuple)):
+        raise ValueError("fill=True takes one device")
+    return name.replace("_batch_", "_fill_")
+
+
+def checksum_host_uniform(data: np.ndarray, stride: int, length: int, n: int, mode="raw", *,
+                          initial: int = 0, initial_arr: np.ndarray | None = None,
+                          addrs: np.ndarray | None = None, out: np.ndarray | None = None,
+                          device: int | list[int] = 0, fill: bool = False) -> np.ndarray:
+    """Host-memory batch in, host-memory results out (pinned staging + pipelined
+    H2D/kernel/D2H inside the library). ``data`` may be a numpy array or a pinned
+    torch CPU tensor (then the copy engine reads it directly). ``device`` may be a
+    list of device indices: one shard per GPU, all at once. ``fill=True`` (TX modes)
+    also stores each result into the packet's checksum field in ``data``
+    (yu_csum_fill_host_uniform)."""
+    m = _mode(mode)
+    data, dptr, dlen = _host_data(data, fill)
     if n and (n - 1) * stride + length > dlen:
         raise ValueError("data too small for the batch geometry")
     ia = None if initial_arr is None else np.ascontiguousarray(initial_arr, dtype=np.uint16)
@@ -175,7 +195,7 @@ def checksum_host_uniform(data: np.ndarray, stride: int, length: int, n: int, mo
         optr = out.ctypes.data
     args = (dptr, stride, length, n, m, None if ia is None else ia.ctypes.data, initial & 0xFFFF,
             None if ad is None else ad.ctypes.data, optr)
-    _host_call("yu_csum_batch_host_uniform", args, device)
+    _host_call(_fill_name("yu_csum_batch_host_uniform", fill, device), args, device)
     return out
 
 
@@ -206,17 +226,12 @@ def _host_side(n, initial_arr, addrs, out):
 
 def checksum_host_ragged(data, offsets, mode="raw", *, initial: int = 0, initial_arr=None,
                          addrs=None, out: np.ndarray | None = None,
-                         device: int | list[int] = 0) -> np.ndarray:
+                         device: int | list[int] = 0, fill: bool = False) -> np.ndarray:
     """Ragged host batch (packet i = data[offsets[i]:offsets[i+1]], e.g. a tun read
-    burst) through the pinned, pipelined host path (yu_csum_batch_host_ragged)."""
+    burst) through the pinned, pipelined host path (yu_csum_batch_host_ragged).
+    ``fill=True``: also the fields, in place (yu_csum_fill_host_ragged)."""
     m = _mode(mode)
-    if isinstance(data, torch.Tensor):
-        if data.is_cuda or data.dtype != torch.uint8 or not data.is_contiguous():
-            raise TypeError("data must be a contiguous uint8 CPU tensor")
-        dptr, dlen = data.data_ptr(), data.numel()
-    else:
-        data = np.ascontiguousarray(data, dtype=np.uint8)
-        dptr, dlen = data.ctypes.data, data.size
+    data, dptr, dlen = _host_data(data, fill)
     offs = np.ascontiguousarray(offsets, dtype=np.uint64)
     n = offs.size - 1
     if n < 0:
@@ -226,16 +241,18 @@ def checksum_host_ragged(data, offsets, mode="raw", *, initial: int = 0, initial
     ia, ad, out = _host_side(n, initial_arr, addrs, out)
     args = (dptr, offs.ctypes.data, n, m, None if ia is None else ia.ctypes.data, initial & 0xFFFF,
             None if ad is None else ad.ctypes.data, out.ctypes.data)
-    _host_call("yu_csum_batch_host_ragged", args, device)
+    _host_call(_fill_name("yu_csum_batch_host_ragged", fill, device), args, device)
     return out
 
 
 def checksum_host_iov(packets, mode="raw", *, initial: int = 0, initial_arr=None, addrs=None,
                       out: np.ndarray | None = None,
-                      device: int | list[int] = 0) -> np.ndarray:
+                      device: int | list[int] = 0, fill: bool = False) -> np.ndarray:
     """Scatter-gather host packets: ``packets[i]`` is a list of views (numpy uint8
     arrays / bytes) whose concatenation is packet i, as tundev's readv fills them
-    (link/tundev/tundev.go:116-125). Gathered into pinned staging by the library."""
+    (link/tundev/tundev.go:116-125). Gathered into pinned staging by the library.
+    ``fill=True``: the fields are written through the views, which must then be
+    writable contiguous uint8 numpy arrays or bytearrays (yu_csum_fill_host_iov)."""
     from ._lib import YuIovec
     m = _mode(mode)
     n = len(packets)
@@ -243,8 +260,14 @@ def checksum_host_iov(packets, mode="raw", *, initial: int = 0, initial_arr=None
     first = np.zeros(n + 1, np.uint64)
     for i, pk in enumerate(packets):
         for v in pk:
-            a = np.frombuffer(v, np.uint8) if isinstance(v, (bytes, bytearray)) else \
-                np.ascontiguousarray(v, dtype=np.uint8)
+            if fill:
+                a = np.frombuffer(v, np.uint8) if isinstance(v, bytearray) else v
+                if not (isinstance(a, np.ndarray) and a.dtype == np.uint8 and a.flags.c_contiguous
+                        and a.flags.writeable):
+                    raise TypeError("fill=True needs writable contiguous uint8 views")
+            else:
+                a = np.frombuffer(v, np.uint8) if isinstance(v, (bytes, bytearray)) else \
+                    np.ascontiguousarray(v, dtype=np.uint8)
             keep.append(a)
             views.append((a.ctypes.data if a.size else None, a.size))
         first[i + 1] = len(views)
@@ -252,7 +275,7 @@ def checksum_host_iov(packets, mode="raw", *, initial: int = 0, initial_arr=None
     ia, ad, out = _host_side(n, initial_arr, addrs, out)
     args = (ctypes_addr(iov), first.ctypes.data, n, m, None if ia is None else ia.ctypes.data,
             initial & 0xFFFF, None if ad is None else ad.ctypes.data, out.ctypes.data)
-    _host_call("yu_csum_batch_host_iov", args, device)
+    _host_call(_fill_name("yu_csum_batch_host_iov", fill, device), args, device)
     del keep
     return out
 

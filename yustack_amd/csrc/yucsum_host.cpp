@@ -777,3 +777,124 @@ extern "C" int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t 
                                   h_addrs ? h_addrs + 8 * a : nullptr, h_out + a, devices[i]);
   });
 }
+
+// ---------------------------------------------------------------------
+// Host-memory field writer (SURVEY.md §8f row 3 for packets in host memory):
+// the batch runs through the host path above, then the CPU stores each TX
+// result big-endian into the packet's checksum field (UDP.SetChecksum
+// header/udp.go:60-62, TCP.SetChecksum header/tcp.go:156-158,
+// IPv4.SetChecksum header/ipv4.go:165-167, ICMPv4.SetChecksum
+// header/icmpv4.go:46-48). The results cross PCIe as 2 bytes per packet
+// either way; writing the fields on the GPU would send every packet back.
+// The same rule as the device writer decides when a field is stored: it must
+// lie inside the packet (IPv4: inside min(len, IHL*4)).
+// ---------------------------------------------------------------------
+namespace {
+
+bool tx_mode(int m) {
+  return m == YU_MODE_UDP || m == YU_MODE_TCP || m == YU_MODE_IPV4 || m == YU_MODE_ICMP;
+}
+
+uint32_t field_offset(int m) {
+  switch (m) {
+    case YU_MODE_UDP: return 6;
+    case YU_MODE_TCP: return 16;
+    case YU_MODE_IPV4: return 10;
+    default: return 2;  // ICMP
+  }
+}
+
+// Byte k of packet i, through a layout's accessor (nullptr past the packet).
+// set(i) writes packet i's field; the packets are split over the copy pool.
+template <class At>
+void set_fields(uint64_t n, int mode, const uint16_t *res, const At &at) {
+  const uint32_t f = field_offset(mode);
+  auto one = [&](uint64_t i) {
+    uint8_t *hi = at(i, f), *lo = at(i, f + 1);
+    if (!hi || !lo) return;
+    if (mode == YU_MODE_IPV4) {  // the field must lie inside the header
+      const uint8_t *b0 = at(i, 0);
+      if (!b0 || (uint32_t)(*b0 & 0xFu) * 4u < f + 2u) return;
+    }
+    *hi = (uint8_t)(res[i] >> 8);
+    *lo = (uint8_t)res[i];
+  };
+  constexpr uint64_t kParMin = 1u << 16;
+  CopyPool &pool = CopyPool::get();
+  const uint64_t parts = std::min<uint64_t>((uint64_t)pool.threads() + 1, n / kParMin);
+  if (parts >= 2) {
+    const uint64_t per = (n + parts - 1) / parts;
+    if (pool.run((int)parts, [&](int k) {
+          for (uint64_t i = (uint64_t)k * per; i < n && i < (uint64_t)(k + 1) * per; ++i) one(i);
+        }))
+      return;
+  }
+  for (uint64_t i = 0; i < n; ++i) one(i);
+}
+
+// Results into the caller's array, or a scratch one when it passes none.
+struct ResultBuf {
+  std::vector<uint16_t> tmp;
+  uint16_t *p;
+  ResultBuf(uint16_t *out, uint64_t n) : p(out) {
+    if (!p) {
+      tmp.resize(n ? n : 1);
+      p = tmp.data();
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" int yu_csum_fill_host_uniform(uint8_t *h_data, uint64_t stride, uint32_t len,
+                                         uint64_t n, int mode, const uint16_t *h_initial_arr,
+                                         uint16_t initial, const uint8_t *h_addrs,
+                                         uint16_t *h_out, int device) {
+  if (!tx_mode(mode)) return YU_EINVAL;
+  if (n == 0) return YU_OK;
+  ResultBuf r(h_out, n);
+  int rc = yu_csum_batch_host_uniform(h_data, stride, len, n, mode, h_initial_arr, initial,
+                                      h_addrs, r.p, device);
+  if (rc) return rc;
+  set_fields(n, mode, r.p, [&](uint64_t i, uint32_t k) -> uint8_t * {
+    return k < len ? h_data + i * stride + k : nullptr;
+  });
+  return YU_OK;
+}
+
+extern "C" int yu_csum_fill_host_ragged(uint8_t *h_data, const uint64_t *h_offsets, uint64_t n,
+                                        int mode, const uint16_t *h_initial_arr,
+                                        uint16_t initial, const uint8_t *h_addrs,
+                                        uint16_t *h_out, int device) {
+  if (!tx_mode(mode)) return YU_EINVAL;
+  if (n == 0) return YU_OK;
+  ResultBuf r(h_out, n);
+  int rc = yu_csum_batch_host_ragged(h_data, h_offsets, n, mode, h_initial_arr, initial, h_addrs,
+                                     r.p, device);
+  if (rc) return rc;
+  set_fields(n, mode, r.p, [&](uint64_t i, uint32_t k) -> uint8_t * {
+    return k < h_offsets[i + 1] - h_offsets[i] ? h_data + h_offsets[i] + k : nullptr;
+  });
+  return YU_OK;
+}
+
+extern "C" int yu_csum_fill_host_iov(const yu_iovec *iov, const uint64_t *first_iov, uint64_t n,
+                                     int mode, const uint16_t *h_initial_arr, uint16_t initial,
+                                     const uint8_t *h_addrs, uint16_t *h_out, int device) {
+  if (!tx_mode(mode)) return YU_EINVAL;
+  if (n == 0) return YU_OK;
+  ResultBuf r(h_out, n);
+  int rc = yu_csum_batch_host_iov(iov, first_iov, n, mode, h_initial_arr, initial, h_addrs, r.p,
+                                  device);
+  if (rc) return rc;
+  // byte k of packet i: walk its views (the field may straddle two of them)
+  set_fields(n, mode, r.p, [&](uint64_t i, uint32_t k) -> uint8_t * {
+    uint64_t at = k;
+    for (uint64_t v = first_iov[i]; v < first_iov[i + 1]; ++v) {
+      if (at < iov[v].len) return (uint8_t *)iov[v].base + at;
+      at -= iov[v].len;
+    }
+    return nullptr;
+  });
+  return YU_OK;
+}
