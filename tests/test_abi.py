@@ -143,8 +143,11 @@ def test_python_front_end_refuses_cpu_tensors():
 
 
 @pytest.mark.parametrize("stride,length,mode,align,want", [
-    (64, 64, "raw", 0, "k_tiny<4>"),
-    (64, 64, "udp", 0, "k_tiny<4>"),         # TX field masked in k_tiny
+    (64, 64, "raw", 0, "k_lane<4>"),
+    (64, 64, "udp", 0, "k_lane<4>"),         # TX field masked by subtraction
+    (20, 20, "raw", 0, "k_lane<2>"),
+    (8, 8, "udp", 0, "k_lane<2>"),           # strides up to 32 bytes
+    (64, 20, "raw", 0, "k_tiny<4>"),         # sparse: k_lane would load 3x the bytes
     (64, 64, "udp", 1, "k_small<8,1>"),      # unaligned start: head junk -> k_small (67 > 64)
     (128, 120, "verify_tcp", 0, "k_tiny<8>"),   # > 112 bytes: every k_tiny<8> lane loads
     (128, 100, "raw", 0, "k_lane<8>"),          # 64 whole strides per wave step in LDS

@@ -80,21 +80,26 @@ def test_transport_uniform(dev, oracle_c, mode, length):
 @pytest.mark.parametrize("mode", [O.MODE_RAW, O.MODE_UDP, O.MODE_TCP, O.MODE_ICMP,
                                   O.MODE_VERIFY_TCP, O.MODE_VERIFY_UDP])
 def test_lane_kernel_shapes(dev, oracle_c, mode):
-    """k_lane (65..112-byte uniform packets, strides to 128): tails of 1-3 bytes,
+    """k_lane (dense uniform packets up to 112 bytes, strides to 128): tails of 1-3 bytes,
     gaps between packets (stride > len), every LDS read width, partial last wave
     steps, and the TX field; k_tiny<8> takes over above 112 bytes."""
     rng = np.random.default_rng(3000 + mode)
     use_addrs = mode in (O.MODE_UDP, O.MODE_TCP, O.MODE_VERIFY_TCP, O.MODE_VERIFY_UDP)
     seen = set()
-    for length, stride in ((65, 68), (66, 68), (67, 68), (68, 68), (71, 72), (72, 72), (72, 80),
+    lo = {O.MODE_UDP: 8, O.MODE_TCP: 20, O.MODE_VERIFY_TCP: 20, O.MODE_VERIFY_UDP: 8, O.MODE_ICMP: 4}
+    for length, stride in ((3, 4), (8, 8), (20, 20), (21, 24), (33, 36), (48, 48), (60, 64), (64, 64),
+                           (65, 68), (66, 68), (67, 68), (68, 68), (71, 72), (72, 72), (72, 80),
                            (80, 80), (81, 96), (96, 96), (100, 100), (104, 104), (112, 112),
                            (100, 128), (112, 128), (127, 128), (128, 128)):
+        if length < lo.get(mode, 1):
+            continue
         seen.add(batch.variant(stride, length, mode, 0))
         for n in (1, 63, 64, 65, 1000):
             got, want = _uniform_case(dev, oracle_c, rng, length, stride, n, mode,
                                       use_addrs=use_addrs, use_init_arr=not use_addrs)
             assert np.array_equal(got, want), (mode, length, stride, n)
-    assert seen == {"k_lane<5>", "k_lane<6>", "k_lane<7>", "k_lane<8>", "k_tiny<8>"}, seen
+    assert {"k_lane<2>", "k_lane<3>", "k_lane<4>", "k_lane<5>", "k_lane<6>", "k_lane<7>", "k_lane<8>",
+            "k_tiny<8>"} <= seen, seen
 
 
 def test_lane_kernel_grid_stride(dev, oracle_c):
@@ -273,7 +278,7 @@ def test_raw_uint32_wrap(dev, oracle_c):
     assert got[0] == 65534  # the reference's wrapped value (exact sum would give 65535)
 
 
-@pytest.mark.parametrize("L", [1500, 124, 100, 72, 64, 20])  # k_small / k_hdr, k_tiny<8>, k_lane<7>, k_lane<5>, k_tiny<4>
+@pytest.mark.parametrize("L", [1500, 124, 100, 72, 64, 20])  # k_small / k_hdr, k_tiny<8>, k_lane<7,5,4,2>
 @pytest.mark.parametrize("mode", [O.MODE_UDP, O.MODE_TCP, O.MODE_IPV4, O.MODE_ICMP])
 def test_fill_in_place(dev, oracle_c, mode, L):
     """fill=True writes the TX field (SetChecksum); re-verifying gives 0/0xFFFF."""

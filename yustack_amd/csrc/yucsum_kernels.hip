@@ -1675,7 +1675,8 @@ const Variant kTiny[] = {YU_TINY(4, (k_tiny<4, 1, true>)), YU_TINY(8, nullptr)};
 // window = the largest stride a wave step's U KiB hold (64 packets)
 #define YU_LANE(U) \
   {"k_lane<" #U ">", 16u * U, {k_lane<U, 0>, k_lane<U, 1>, k_lane<U, 1>}, 1, 64u}
-const Variant kLane[] = {YU_LANE(5), YU_LANE(6), YU_LANE(7), YU_LANE(8)};
+const Variant kLane[] = {YU_LANE(2), YU_LANE(3), YU_LANE(4),
+                         YU_LANE(5), YU_LANE(6), YU_LANE(7), YU_LANE(8)};
 
 // Ordered by window; for each window the variant with the most packets per
 // wave comes first (amortises the per-packet epilogue over more bytes).
@@ -1740,9 +1741,11 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
   };
   // k_tiny: no junk bytes (4-aligned starts, no TX field, no IPv4 header walk)
   const bool tiny_ok = aligned4 && !mode_is_ipv4(mode) && mode != YU_MODE_VERIFY_RX;
-  // k_lane: the same modes, one wave step = 64 whole strides in LDS
+  // k_lane: the same modes, one wave step = 64 whole strides in LDS, so only
+  // where gaps between packets waste at most half the bytes it loads
   auto lane_fits = [&](const Variant &v) {
-    return tiny_ok && (stride & 3u) == 0 && len <= stride && stride <= v.window;
+    return tiny_ok && (stride & 3u) == 0 && len >= 1u && len <= stride && stride <= v.window &&
+           2u * stride <= 3u * (uint64_t)len;
   };
   if (mode == YU_MODE_VERIFY_RX) return pick_ragged(mode);
   // IPv4 header-only modes: one lane per packet (1M x 1500-B datagrams:
@@ -1758,10 +1761,10 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
     for (const Variant &v : kLane)
       if (strcmp(v.name, f) == 0 && lane_fits(v)) return v;
   }
-  // k_tiny<4> up to 64 bytes, k_lane to 112 (72-byte UDP datagrams: 16.4 vs
-  // 20.0 us with k_tiny<8>, 96 bytes: 19.3 vs 21.0), k_tiny<8> above, where
-  // all its lanes load (128 bytes: 23.6 vs 24.6 us; tools/kbench 14)
-  if (tiny_ok && len <= 64u && fits(kTiny[0])) return kTiny[0];
+  // k_lane up to 112 bytes (72-byte UDP datagrams: 16.4 vs 20.0 us with
+  // k_tiny<8>; 64-byte packets, config 2: 14.2 vs 14.8 with k_tiny<4>),
+  // k_tiny<8> above, where all its lanes load (128 bytes: 23.6 vs 24.6 us;
+  // tools/kbench 2 and 14); k_tiny<4> for sparse small packets
   if (len <= 112u)
     for (const Variant &v : kLane)
       if (lane_fits(v)) return v;
