@@ -148,12 +148,13 @@ def test_python_front_end_refuses_cpu_tensors():
     (20, 20, "raw", 0, "k_lane<2>"),
     (8, 8, "udp", 0, "k_lane<2>"),           # strides up to 32 bytes
     (64, 20, "raw", 0, "k_tiny<4>"),         # sparse: k_lane would load 3x the bytes
-    (64, 64, "udp", 1, "k_small<8,1>"),      # unaligned start: head junk -> k_small (67 > 64)
+    (64, 64, "udp", 1, "k_seg<4,tx>"),       # unaligned dense: the segmented stream sum
     (128, 120, "verify_tcp", 0, "k_tiny<8>"),   # > 112 bytes: every k_tiny<8> lane loads
     (128, 100, "raw", 0, "k_lane<8>"),          # 64 whole strides per wave step in LDS
     (100, 100, "tcp", 0, "k_lane<7>"),
     (72, 72, "udp", 0, "k_lane<5>"),            # sendUDP datagram: 8-B header + 64-B payload
-    (72, 70, "raw", 2, "k_small<8,1>"),         # unaligned: no k_lane
+    (72, 70, "raw", 2, "k_seg<4>"),             # unaligned: no k_lane
+    (256, 70, "raw", 2, "k_small<8,1>"),        # unaligned and sparse
     (136, 128, "raw", 0, "k_tiny<8>"),          # stride > 128: no k_lane
     (1500, 1500, "tcp", 0, "k_small<16,6>"),
     (1500, 1500, "tcp", 2, "k_small<16,6>"),     # 1503 still fits 1536
@@ -161,8 +162,11 @@ def test_python_front_end_refuses_cpu_tensors():
     (9000, 9000, "raw", 0, "k_loop<4,LE>"),
     (200000, 200000, "raw", 0, "k_loop<4,BE>"),  # > 131072: exact uint32 wrap path
     (1500, 1500, "ipv4", 0, "k_hdr"),            # only the <= 60-byte header is read
-    (20, 20, "udp", 3, "k_small<4,1>"),
-    (62, 62, "raw", 1, "k_small<8,1>"),      # 65 > 64
+    (20, 20, "udp", 3, "k_seg<4,tx>"),
+    (320, 320, "tcp", 0, "k_seg<4,tx>"),        # 129..704 B dense
+    (512, 512, "raw", 0, "k_seg<8>"),
+    (62, 62, "raw", 1, "k_seg<4>"),
+    (200, 62, "raw", 1, "k_small<8,1>"),     # sparse: 65 > 64
 ])
 def test_variant_selection(stride, length, mode, align, want):
     assert batch.variant(stride, length, mode, align) == want

@@ -1771,11 +1771,13 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
   if (tiny_ok)
     for (const Variant &v : kTiny)
       if (fits(v)) return v;
-  // 129..704-byte dense packets: the segmented stream sum beats per-packet lane
+  // Dense packets up to 704 bytes that k_lane / k_tiny do not take (129..704
+  // bytes, or not 4-aligned): the segmented stream sum beats per-packet lane
   // groups, whose loads scatter over partly used windows (160 B: 34.6 vs 50.0 us;
-  // 320: 58-66 vs 88-89; 512: 87 vs 103; 704: 116 vs 120; from 768 on k_small
-  // is as fast or faster; tools/kbench 14, profiles/r01/kbench_uniform_size_sweep.log)
-  if (len > 128u && len <= 704u && 2u * stride <= 3u * (uint64_t)len) return seg_for(len >= 448u, mode);
+  // 320: 58-66 vs 88-89; 512: 87 vs 103; 704: 116 vs 120; unaligned 66 B: 26.8
+  // vs 38.6; from 768 on k_small is as fast or faster; tools/kbench 14,
+  // profiles/r01/kbench_uniform_size_sweep.log)
+  if (len <= 704u && 2u * stride <= 3u * (uint64_t)len) return seg_for(len >= 448u, mode);
   for (const Variant &v : kSmall)
     if (fits(v)) return v;
   return len > kLEMax ? kLoopBE : kLoopLE;
