@@ -304,6 +304,10 @@ int yu_device_count(void);
  * (for profiling and tests; no device needed). Returns a static string. */
 const char *yu_uniform_variant(uint64_t stride, uint32_t len, int mode,
                                uint64_t data_align16);
+/* The same for a batch of n packets (the choice above 3 KiB depends on n;
+ * yu_uniform_variant answers for n = 2). */
+const char *yu_uniform_variant_n(uint64_t stride, uint32_t len, uint64_t n,
+                                 int mode, uint64_t data_align16);
 /* Name of the kernel variant the ragged path launches for this mode (static
  * string; "" for a bad mode). */
 const char *yu_ragged_variant(int mode);

@@ -877,3 +877,21 @@ def test_host_fill_paths(dev, oracle_c):
     check(flat, after, offs[:-1].astype(np.int64), want, O.MODE_UDP)
     with pytest.raises(TypeError):
         batch.checksum_host_iov([[bytes(8)]], "udp", fill=True)
+
+
+def test_uniform_large_dense_batches_take_k_seg(dev, oracle_c):
+    """Dense uniform packets above 3 KiB in a large batch run on k_seg (8 KiB
+    tiles): parity for TCP segments and RAW packets with a per-packet initial."""
+    rng = np.random.default_rng(31)
+    for L, mode, n in ((4100, O.MODE_TCP, 70_000), (9001, O.MODE_RAW, 65_536)):
+        assert batch.variant(L, L, mode, 0, n=n) == ("k_seg<8,tx>" if mode == O.MODE_TCP else "k_seg<8>")
+        host = _rand(rng, n * L)
+        if mode == O.MODE_TCP:
+            host[12::L] = 0x50
+        addrs = _rand(rng, 8 * n) if mode == O.MODE_TCP else None
+        init = rng.integers(0, 65536, size=n, dtype=np.uint16) if mode == O.MODE_RAW else None
+        got = batch.checksum_uniform(_to(dev, host), L, L, n, mode,
+                                     addrs=None if addrs is None else _to(dev, addrs),
+                                     initial_arr=None if init is None else _to(dev, init)).cpu().numpy()
+        want = oracle_c.batch(host, mode, stride=L, length=L, n=n, addrs=addrs, initial_arr=init, threads=8)
+        assert np.array_equal(got, want), (L, mode)

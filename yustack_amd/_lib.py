@@ -21,7 +21,7 @@ EXPORTS = (
     "yu_csum_batch_host_uniform_multi", "yu_csum_batch_host_ragged_multi",
     "yu_csum_batch_host_iov_multi",
     "yu_csum_fill_host_uniform", "yu_csum_fill_host_ragged", "yu_csum_fill_host_iov",
-    "yu_abi_version", "yu_strerror", "yu_device_count", "yu_uniform_variant",
+    "yu_abi_version", "yu_strerror", "yu_device_count", "yu_uniform_variant", "yu_uniform_variant_n",
     "yu_ragged_variant",
 )
 
@@ -94,6 +94,8 @@ def lib() -> ctypes.CDLL:
     L.yu_device_count.argtypes = []
     L.yu_uniform_variant.restype = c.c_char_p
     L.yu_uniform_variant.argtypes = [u64, u32, i32, u64]
+    L.yu_uniform_variant_n.restype = c.c_char_p
+    L.yu_uniform_variant_n.argtypes = [u64, u32, u64, i32, u64]
     L.yu_ragged_variant.restype = c.c_char_p
     L.yu_ragged_variant.argtypes = [i32]
     del u8

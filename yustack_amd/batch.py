@@ -305,6 +305,7 @@ def ragged_variant(mode="raw") -> str:
     return lib().yu_ragged_variant(_mode(mode)).decode()
 
 
-def variant(stride: int, length: int, mode="raw", align16: int = 0) -> str:
-    """Name of the kernel the uniform path launches for this geometry."""
-    return lib().yu_uniform_variant(stride, length, _mode(mode), align16).decode()
+def variant(stride: int, length: int, mode="raw", align16: int = 0, n: int = 2) -> str:
+    """Name of the kernel the uniform path launches for this geometry (and batch
+    size: dense packets above 3 KiB go to k_seg only in large batches)."""
+    return lib().yu_uniform_variant_n(stride, length, n, _mode(mode), align16).decode()
