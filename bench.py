@@ -143,7 +143,7 @@ class Workload:
 
     def kernel_name(self) -> str:
         if self.offsets is not None:
-            return batch.ragged_variant(self.mode)
+            return batch.ragged_variant(self.mode, self.n)
         return batch.variant(self.L, self.L, self.mode, self.data[0].data_ptr() & 15, n=self.n)
 
 

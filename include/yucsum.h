@@ -309,8 +309,10 @@ const char *yu_uniform_variant(uint64_t stride, uint32_t len, int mode,
 const char *yu_uniform_variant_n(uint64_t stride, uint32_t len, uint64_t n,
                                  int mode, uint64_t data_align16);
 /* Name of the kernel variant the ragged path launches for this mode (static
- * string; "" for a bad mode). */
+ * string; "" for a bad mode), for a large batch; _n: for a batch of n
+ * packets (bursts of up to 4096 packets take a wave per packet). */
 const char *yu_ragged_variant(int mode);
+const char *yu_ragged_variant_n(int mode, uint64_t n);
 
 #ifdef __cplusplus
 }

@@ -130,12 +130,15 @@ def _ragged(rng, lens, base_off=0, kind="rand"):
     return _rand(rng, int(offs[-1]) + 32, kind), offs
 
 
+@pytest.mark.parametrize("npk", [600, 4500])  # a small burst (k_loop) and k_seg
 @pytest.mark.parametrize("mode", list(range(8)))
-def test_ragged_all_modes(dev, oracle_c, mode):
-    rng = np.random.default_rng(3000 + mode)
+def test_ragged_all_modes(dev, oracle_c, mode, npk):
+    rng = np.random.default_rng(3000 + mode + npk)
     lo = {O.MODE_UDP: 8, O.MODE_TCP: 60, O.MODE_VERIFY_TCP: 60, O.MODE_ICMP: 4,
           O.MODE_IPV4: 60, O.MODE_VERIFY_IPV4: 60}.get(mode, 0)
-    lens = rng.integers(lo, 9001, size=600)
+    if mode not in (O.MODE_IPV4, O.MODE_VERIFY_IPV4):
+        assert batch.ragged_variant(mode, npk).startswith("k_loop" if npk <= 4096 else "k_seg")
+    lens = rng.integers(lo, 9001, size=npk)
     lens[:len(EDGE_LENS)] = np.maximum(np.array(EDGE_LENS), lo)
     blob, offs = _ragged(rng, lens, base_off=3)
     n = len(lens)
@@ -759,7 +762,7 @@ def test_random_batches_fuzz(dev, oracle_c):
     for it in range(800):
         mode = int(rng.integers(0, 8))  # VERIFY_RX has its own tests (real headers)
         lo = _MIN_LEN.get(mode, 0)
-        n = int(rng.choice([1, 2, 63, 64, 65, int(rng.integers(1, 3000))]))
+        n = int(rng.choice([1, 2, 63, 64, 65, int(rng.integers(1, 3000)), int(rng.integers(4097, 6000))]))
         ragged = bool(rng.integers(0, 2))
         side = int(rng.integers(0, 3))  # 0: scalar initial, 1: initial_arr, 2: addrs
         tx = mode in _FIELD or mode == O.MODE_IPV4
@@ -777,7 +780,7 @@ def test_random_batches_fuzz(dev, oracle_c):
             _fuzz_headers(rng, blob, offs[:-1], lens, mode)
             want = oracle_c.batch(blob, mode, offsets=offs, initial_arr=init, initial=initial, addrs=addrs)
             d = _to(dev, blob)
-            seen.add(batch.ragged_variant(mode))
+            seen.add(batch.ragged_variant(mode, n))
             got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), mode, initial=initial,
                                         initial_arr=None if init is None else _to(dev, init),
                                         addrs=None if addrs is None else _to(dev, addrs),

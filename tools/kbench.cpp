@@ -56,7 +56,8 @@ int main(int argc, char **argv) {
   std::vector<int> cfgs;
   for (int i = 1; i < argc; ++i) cfgs.push_back(atoi(argv[i]));
   if (cfgs.empty()) cfgs = {2, 3, 4};
-  const uint64_t n = 1ull << 20;
+  // KB_N: packets per batch (default 1M)
+  const uint64_t n = getenv("KB_N") ? strtoull(getenv("KB_N"), nullptr, 10) : 1ull << 20;
   const int reps = 30, rounds = 3;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -146,7 +147,7 @@ int main(int argc, char **argv) {
       double s = ms / 1e3 / reps;
       printf("config%d round %d: %8.1f us/launch  %7.1f GB/s alg  (%.3f of 8 TB/s)  %s\n", cfg, r, s * 1e6,
              alg / s / 1e9, alg / s / 8e12,
-             d_off ? yu_ragged_variant(mode)
+             d_off ? yu_ragged_variant_n(mode, n)
                    : yu_uniform_variant_n(L, L, n, mode, (uintptr_t)bufs[0] & 15));
     }
     for (auto b : bufs) CK(hipFree(b));

@@ -300,9 +300,10 @@ def rx_accepted(flags: torch.Tensor) -> torch.Tensor:
     return ok_ip & ok_l4
 
 
-def ragged_variant(mode="raw") -> str:
-    """Name of the kernel the ragged path launches for this mode."""
-    return lib().yu_ragged_variant(_mode(mode)).decode()
+def ragged_variant(mode="raw", n: int = 1 << 20) -> str:
+    """Name of the kernel the ragged path launches for this mode and batch size
+    (bursts of up to 4096 packets take a wave per packet)."""
+    return lib().yu_ragged_variant_n(_mode(mode), n).decode()
 
 
 def variant(stride: int, length: int, mode="raw", align16: int = 0, n: int = 2) -> str:

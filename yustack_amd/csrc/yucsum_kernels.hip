@@ -1712,13 +1712,25 @@ const Variant &seg_for(bool u8, int mode) {
 // windows). 8 KiB tiles beat 4 KiB ones from ~800-byte packets up (config 4:
 // 84.9 vs 83.4 % of peak, U{64..1500}: 80.5 vs 77.7 %) and lose below
 // (U{40..200}: 54 vs 61-66 %). Measurement override YU_RAGGED=loop|rag|seg4|seg8.
-const Variant &pick_ragged(int mode) {
+// Small bursts (n <= kSmallBurst, e.g. a tun read burst on the host path) go to
+// k_loop instead: k_seg gives each 64-packet chunk to one wave, which streams
+// the chunk's tiles one after another, so a burst of few chunks leaves the GPU
+// idle and pays one memory latency per tile. One wave per packet instead
+// (tools/kbench KB_N, profiles/r01/kbench_ragged_burst_size.log): 64 packets of
+// U{64..1500} 8.6 -> 3.4 us, 1024 of them 10.7 -> 3.8, 2048 jumbo packets
+// U{64..9000} 43.2 -> 5.7; at 4096 small packets U{40..200} the two tie (4.7);
+// from 16384 packets on k_seg wins on small packets (5.4 vs 11.5).
+constexpr uint64_t kSmallBurst = 4096;
+
+const Variant &pick_ragged(int mode, uint64_t n) {
   static const char *f = getenv("YU_RAGGED");
   const bool seg4 = f && strcmp(f, "seg4") == 0;
   const bool rx = mode == YU_MODE_VERIFY_RX;  // only k_seg verifies whole datagrams
-  if (f && strcmp(f, "loop") == 0 && !rx) return mode == YU_MODE_RAW ? kLoopBE : kLoopLE;
+  const Variant &loop = mode == YU_MODE_RAW ? kLoopBE : kLoopLE;  // BE: exact past 131072 B
+  if (f && strcmp(f, "loop") == 0 && !rx) return loop;
   if (f && strcmp(f, "rag") == 0 && !rx) return kRag;
   if (mode_is_ipv4(mode)) return kHdr;  // header-only: one lane per packet
+  if (!rx && n <= kSmallBurst && !f) return loop;
   return seg_for(!seg4, mode);
 }
 
@@ -1747,7 +1759,7 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
     return tiny_ok && (stride & 3u) == 0 && len >= 1u && len <= stride && stride <= v.window &&
            2u * stride <= 3u * (uint64_t)len;
   };
-  if (mode == YU_MODE_VERIFY_RX) return pick_ragged(mode);
+  if (mode == YU_MODE_VERIFY_RX) return pick_ragged(mode, n);
   // IPv4 header-only modes: one lane per packet (1M x 1500-B datagrams:
   // 29.9 us vs 36.9 with k_small<4,1>, kbench 13)
   if (mode_is_ipv4(mode) && !forced_variant()) return kHdr;
@@ -1946,7 +1958,7 @@ int batch_ragged(const uint8_t *data, uint8_t *fill, const uint64_t *offsets,
   A.mode = mode;
   // k_seg streams the batch's bytes (exact BE recovery for chunks holding a
   // RAW packet > 131072 bytes); k_rag takes the IPv4 header-only modes.
-  return launch(pick_ragged(mode), A, (hipStream_t)stream);
+  return launch(pick_ragged(mode, n), A, (hipStream_t)stream);
 }
 
 // Completion signal for the host path's direct mode (yucsum_internal.h):
@@ -2015,7 +2027,12 @@ const char *yu_uniform_variant_n(uint64_t stride, uint32_t len, uint64_t n, int 
 
 const char *yu_ragged_variant(int mode) {
   if (mode < 0 || mode >= YU_MODE_COUNT) return "";
-  return pick_ragged(mode).name;
+  return pick_ragged(mode, 1u << 20).name;
+}
+
+const char *yu_ragged_variant_n(int mode, uint64_t n) {
+  if (mode < 0 || mode >= YU_MODE_COUNT) return "";
+  return pick_ragged(mode, n).name;
 }
 
 int yu_device_count(void) {
