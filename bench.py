@@ -299,6 +299,24 @@ def end_to_end(w: Workload, reps: int = 3):
         for _ in range(k):
             batch.checksum_host_uniform(src, w.L, w.L, bn, w.mode, initial_arr=ia, addrs=ad, out=o)
         res[f"burst{bn}_pinned_us_per_call"] = round((time.perf_counter() - t0) / k * 1e6, 1)
+    # tun RX bursts: whole IPv4 datagrams U{40..1500} B back to back in pinned
+    # memory, verified (VERIFY_RX) through the ragged host path
+    rng = np.random.default_rng(5)
+    for bn in (64, 1024):
+        lens = rng.integers(40, 1501, size=bn)
+        offs = np.zeros(bn + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+        blob = torch.from_numpy(rng.integers(0, 256, size=int(offs[-1]), dtype=np.uint8)).pin_memory()
+        b, s0 = blob.numpy(), offs[:-1]
+        b[s0], b[s0 + 2], b[s0 + 3], b[s0 + 9] = 0x45, lens >> 8, lens & 0xFF, 6
+        o = np.empty(bn, np.uint16)
+        for _ in range(10):
+            batch.checksum_host_ragged(blob, offs, "verify_rx", out=o)
+        k = 300
+        t0 = time.perf_counter()
+        for _ in range(k):
+            batch.checksum_host_ragged(blob, offs, "verify_rx", out=o)
+        res[f"rx_burst{bn}_pinned_us_per_call"] = round((time.perf_counter() - t0) / k * 1e6, 1)
     ndev = torch.cuda.device_count()
     if ndev > 1:  # yu_csum_batch_host_uniform_multi: one shard per visible GPU, each on its own PCIe link
         devs = list(range(ndev))

@@ -215,13 +215,15 @@ def test_ragged_far_from_step_base(dev, oracle_c, mode):
     assert np.array_equal(got, want), np.nonzero(got != want)[0]
 
 
+@pytest.mark.parametrize("npk", [3000, 4500])  # a burst (k_loop_rx) and k_seg's RX kind
 @pytest.mark.parametrize("lo,hi", [(0, 40), (0, 300), (0, 1480), (1000, 9000)])
-def test_verify_rx_ragged(dev, oracle_c, lo, hi):
+def test_verify_rx_ragged(dev, oracle_c, lo, hi, npk):
     """Whole received datagrams (tun RX bursts): header + transport verification
     bits against the oracle, every start alignment, valid and damaged packets."""
     import rxgen
-    rng = np.random.default_rng(9100 + hi)
-    blob, offs = rxgen.rx_batch(rng, 3000, lo=lo, hi=min(hi, 65535 - 80))
+    assert batch.ragged_variant("verify_rx", npk) == ("k_loop<4,rx>" if npk <= 4096 else "k_seg<8,rx>")
+    rng = np.random.default_rng(9100 + hi + npk)
+    blob, offs = rxgen.rx_batch(rng, npk, lo=lo, hi=min(hi, 65535 - 80))
     for base_off in (0, 1, 2, 3):
         b = np.concatenate([np.zeros(base_off, np.uint8), blob, np.zeros(32, np.uint8)])
         o = offs + base_off
@@ -231,12 +233,13 @@ def test_verify_rx_ragged(dev, oracle_c, lo, hi):
     assert len(np.unique(want)) >= 5
 
 
+@pytest.mark.parametrize("npk", [777, 5000])
 @pytest.mark.parametrize("length", [20, 40, 64, 576, 1500])
-def test_verify_rx_uniform(dev, oracle_c, length):
+def test_verify_rx_uniform(dev, oracle_c, length, npk):
     """Fixed-size received datagrams in uniform slots (stride >= length)."""
     import rxgen
-    rng = np.random.default_rng(9200 + length)
-    n, stride = 777, length + 5
+    rng = np.random.default_rng(9200 + length + npk)
+    n, stride = npk, length + 5
     host = np.zeros(n * stride + 64, np.uint8)
     for p in range(n):
         pk = rxgen.make_packet(rng, length - 20, ihl=5)

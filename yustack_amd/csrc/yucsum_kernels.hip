@@ -1650,6 +1650,95 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
 }
 
 // ---------------------------------------------------------------------
+// k_loop_rx<U, NT>: VERIFY_RX for small bursts, a wave per datagram as in
+// k_loop (k_seg's one wave per 64-packet chunk leaves a burst's GPU idle).
+// Window 0 holds the header: the wave parses it from lanes 0-1's registers,
+// then every dword counts toward the header sum [sh, sh+hl) or the transport
+// sum [sh+hl, sh+tl) through byte masks (window coordinates, base floor4 of
+// the start). Same checks and result bits as k_seg's RX kind.
+// ---------------------------------------------------------------------
+template <int U, int NT>
+__global__ __launch_bounds__(256) void k_loop_rx(BatchArgs A) {
+  constexpr uint32_t W = 64u * 16u * U;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = grid_wave(A.xcd);
+  const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t end = A.offsets ? (uint64_t)(uintptr_t)A.data + A.offsets[A.n] : A.end;
+
+  uint64_t p = wave;
+  if (p >= A.n) return;
+  LoopPkt cur, nxt;
+  loop_pkt(A, p, false, cur);
+  uint64_t pn = p + nwave;
+  loop_pkt(A, pn, false, nxt);
+  uint32_t wb = 0;
+  uint4 c[U];
+  loop_fetch<U, NT>(cur, 0, lane, end, c);
+  uint32_t ah = 0, at = 0, hl = 0, tl = 0;
+  SegRx rx;
+  for (;;) {
+    const bool last = wb + W >= cur.eload;  // wave-uniform
+    const bool more = !last || pn < A.n;
+    uint4 cn[U];
+    loop_fetch<U, NT>(last ? nxt : cur, last ? 0u : wb + W, lane, end, cn);
+    if (wb == 0) {  // header window dwords 0..5: lane 0's chunk, half of lane 1's
+      rx.h[0] = (uint32_t)__builtin_amdgcn_readlane((int)c[0].x, 0);
+      rx.h[1] = (uint32_t)__builtin_amdgcn_readlane((int)c[0].y, 0);
+      rx.h[2] = (uint32_t)__builtin_amdgcn_readlane((int)c[0].z, 0);
+      rx.h[3] = (uint32_t)__builtin_amdgcn_readlane((int)c[0].w, 0);
+      rx.h[4] = (uint32_t)__builtin_amdgcn_readlane((int)c[0].x, 1);
+      rx.h[5] = (uint32_t)__builtin_amdgcn_readlane((int)c[0].y, 1);
+      rx.flags = YU_RX_INVALID;
+      rx.pseudo = 0u;
+      hl = tl = 0u;
+      if (cur.len >= 20u) rx_parse(rx, cur.sh, cur.len, hl, tl);  // IsValid: minimum size
+    }
+    const uint32_t a = cur.sh, b = cur.sh + hl, e = cur.sh + tl;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t w[4] = {c[u].x, c[u].y, c[u].z, c[u].w};
+      const uint32_t base = wb + 16u * (lane + 64u * (uint32_t)u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = base + 4u * (uint32_t)j;
+        ah = sad(w[j] & byte_range_mask(lo, a, b), ah);
+        at = sad(w[j] & byte_range_mask(lo, b, e), at);
+      }
+    }
+    if (last) {
+      ah = group_total<64>(ah);
+      at = group_total<64>(at);
+      if (lane == 63u) {
+        // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
+        // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
+        uint32_t r = rx.flags;
+        if (!(r & YU_RX_INVALID)) {
+          const uint32_t odd = cur.sh & 1u;
+          const uint32_t ip = fold32(le_to_be(ah, odd));
+          if (ip == 0u || ip == 0xFFFFu) r |= YU_RX_IP_OK;
+          if (r & YU_RX_L4) {
+            const uint32_t l4 = fold32(le_to_be(at, odd) + rx.pseudo);
+            if (l4 == 0u || l4 == 0xFFFFu) r |= YU_RX_L4_OK;
+          }
+        }
+        if (A.out) A.out[p] = (uint16_t)r;
+      }
+      if (!more) break;
+      p = pn;
+      cur = nxt;
+      pn = p + nwave;
+      loop_pkt(A, pn, false, nxt);
+      wb = 0;
+      ah = at = 0u;
+    } else {
+      wb += W;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = cn[u];
+  }
+}
+
+// ---------------------------------------------------------------------
 // Host side: variant selection and launch.
 // ---------------------------------------------------------------------
 typedef void (*KernelFn)(BatchArgs);
@@ -1687,6 +1776,7 @@ const Variant kSmall[] = {
 };
 const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, 0, false>, k_loop<4, 1, false>, k_loop<4, 1, false>}, 64, 1};
 const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, 0, true>, k_loop<4, 1, true>, k_loop<4, 1, true>}, 64, 1};
+const Variant kLoopRx = {"k_loop<4,rx>", 0, {k_loop_rx<4, 0>, k_loop_rx<4, 1>, k_loop_rx<4, 1>}, 64, 1};
 const Variant kRag = {"k_rag<16,6>", 1536, {k_rag<16, 6, 0>, k_rag<16, 6, 1>, k_rag<16, 6, 2>}, 16, 4};
 // plain loads by default: for scattered 32-byte header reads they beat nt
 // ones (30.7 vs 32.5 us, kbench 12)
@@ -1719,18 +1809,19 @@ const Variant &seg_for(bool u8, int mode) {
 // (tools/kbench KB_N, profiles/r01/kbench_ragged_burst_size.log): 64 packets of
 // U{64..1500} 8.6 -> 3.4 us, 1024 of them 10.7 -> 3.8, 2048 jumbo packets
 // U{64..9000} 43.2 -> 5.7; at 4096 small packets U{40..200} the two tie (4.7);
-// from 16384 packets on k_seg wins on small packets (5.4 vs 11.5).
+// from 16384 packets on k_seg wins on small packets (5.4 vs 11.5). VERIFY_RX
+// bursts take k_loop_rx, the same shape.
 constexpr uint64_t kSmallBurst = 4096;
 
 const Variant &pick_ragged(int mode, uint64_t n) {
   static const char *f = getenv("YU_RAGGED");
   const bool seg4 = f && strcmp(f, "seg4") == 0;
   const bool rx = mode == YU_MODE_VERIFY_RX;  // only k_seg verifies whole datagrams
-  const Variant &loop = mode == YU_MODE_RAW ? kLoopBE : kLoopLE;  // BE: exact past 131072 B
-  if (f && strcmp(f, "loop") == 0 && !rx) return loop;
+  const Variant &loop = rx ? kLoopRx : (mode == YU_MODE_RAW ? kLoopBE : kLoopLE);  // BE: exact past 131072 B
+  if (f && strcmp(f, "loop") == 0) return loop;
   if (f && strcmp(f, "rag") == 0 && !rx) return kRag;
   if (mode_is_ipv4(mode)) return kHdr;  // header-only: one lane per packet
-  if (!rx && n <= kSmallBurst && !f) return loop;
+  if (n <= kSmallBurst && !f) return loop;
   return seg_for(!seg4, mode);
 }
 
