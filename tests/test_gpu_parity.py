@@ -760,9 +760,11 @@ def test_random_batches_fuzz(dev, oracle_c):
     """Randomised geometry x mode x side data x fill: every kernel variant the
     selection can pick (k_tiny, k_lane, k_small, k_hdr, k_seg, k_loop), against the
     C oracle on the same bytes. Seeded, so a failure reproduces."""
-    rng = np.random.default_rng(2026)
+    import os
+    # YU_FUZZ_SEED / YU_FUZZ_ITERS: longer or different runs by hand
+    rng = np.random.default_rng(int(os.environ.get("YU_FUZZ_SEED", "2026")))
     seen = set()
-    for it in range(800):
+    for it in range(int(os.environ.get("YU_FUZZ_ITERS", "800"))):
         mode = int(rng.integers(0, 8))  # VERIFY_RX has its own tests (real headers)
         lo = _MIN_LEN.get(mode, 0)
         n = int(rng.choice([1, 2, 63, 64, 65, int(rng.integers(1, 3000)), int(rng.integers(4097, 6000))]))
