@@ -44,24 +44,29 @@
 // vmcnt bookkeeping stays exact. That lets the kernels keep the next step's
 // loads in flight while the current step is summed (software pipelining).
 //
-// Work mapping (wave64-first, not a warp tiling):
-//   k_tiny<G>: uniform, packets <= 16G bytes, 4-aligned, no junk bytes: a wave
-//     step covers 64 packets, each load instruction one contiguous KiB, and a
-//     cross-lane transpose lets every lane finish one packet (BASELINE config 2).
-//   k_lane<U>: uniform, 4-aligned, 65..112 bytes (the 72-byte sendUDP
-//     datagram): 64 whole strides per wave step parked in LDS, one lane per
-//     packet summing it from there.
-//   k_small<G, U>: uniform stride, packet span <= G*U*16 bytes. A wave holds
-//     64/G packets per step; each group of G lanes loads its packet window in
-//     U dwordx4 loads per lane, reduces with log2(G) DPP adds and its last
-//     lane finishes the packet (config 3: k_small<16,6>).
-//   k_seg<U, NT, K>: ragged (tun-style, any alignment) batches and VERIFY_RX:
-//     a segmented sum over the byte stream of 64 consecutive packets per wave,
-//     U KiB tiles, packet sums as prefix differences (config 4, tun RX).
+// Work mapping (wave64-first, not a warp tiling). Which kernel a batch gets
+// depends on its layout, mode, packet size and count (pick_uniform /
+// pick_ragged below, each cut-over measured):
+//   k_lane<U>: dense uniform 4-aligned packets up to 112 bytes (configs 2 and
+//     8): 64 whole strides per wave step parked in LDS, one lane per packet
+//     summing it from there.
+//   k_tiny<G>: uniform 4-aligned packets <= 16G bytes that k_lane does not take
+//     (113..128 bytes, sparse small ones): a wave step covers 64 packets, each
+//     load instruction one contiguous KiB, and a cross-lane transpose lets
+//     every lane finish one packet.
+//   k_small<G, U>: uniform stride, packet span <= G*U*16 bytes (705..3072 and
+//     sparse ones). A wave holds 64/G packets per step; each group of G lanes
+//     loads its packet window in U dwordx4 loads per lane, reduces with log2(G)
+//     DPP adds and its last lane finishes the packet (config 3: k_small<16,6>).
+//   k_seg<U, NT, K>: ragged batches of more than 4096 packets, VERIFY_RX, and
+//     dense uniform packets of other sizes: a segmented sum over the byte
+//     stream of 64 consecutive packets per wave, U KiB tiles, packet sums as
+//     prefix differences (config 4, tun RX).
 //   k_hdr<NT>: the IPv4 header-only modes (<= 60 bytes of each packet), uniform
 //     and ragged: one lane per packet, 32-byte reads.
+//   k_loop<U, BE> / k_loop_rx<U>: one wave per packet, for ragged bursts of up
+//     to 4096 packets and for few or sparse uniform packets > 4 KiB.
 //   k_rag<G, U>: the first ragged kernel, kept as a measurement alternative.
-//   k_loop<U, BE>: one wave per packet, for uniform packets > 4 KiB.
 //   All are grid-stride kernels; the grid is sized per CU and over-subscribed
 //   (see blocks_per_cu), except that k_seg narrows it for small packets
 //   (seg_waves).
