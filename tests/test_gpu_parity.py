@@ -221,7 +221,7 @@ def test_verify_rx_ragged(dev, oracle_c, lo, hi, npk):
     """Whole received datagrams (tun RX bursts): header + transport verification
     bits against the oracle, every start alignment, valid and damaged packets."""
     import rxgen
-    assert batch.ragged_variant("verify_rx", npk) == ("k_loop<4,rx>" if npk <= 4096 else "k_seg<8,rx>")
+    assert batch.ragged_variant("verify_rx", npk) == ("k_loop<4,rx>" if npk <= 4096 else "k_seg<8,rx,c16>")
     rng = np.random.default_rng(9100 + hi + npk)
     blob, offs = rxgen.rx_batch(rng, npk, lo=lo, hi=min(hi, 65535 - 80))
     for base_off in (0, 1, 2, 3):
@@ -903,3 +903,28 @@ def test_uniform_large_dense_batches_take_k_seg(dev, oracle_c):
                                      initial_arr=None if init is None else _to(dev, init)).cpu().numpy()
         want = oracle_c.batch(host, mode, stride=L, length=L, n=n, addrs=addrs, initial_arr=init, threads=8)
         assert np.array_equal(got, want), (L, mode)
+
+
+@pytest.mark.parametrize("mode", [O.MODE_RAW, O.MODE_UDP, O.MODE_VERIFY_TCP, O.MODE_VERIFY_RX])
+def test_ragged_batch_size_cutovers(dev, oracle_c, mode):
+    """The same kind of burst at each ragged cut-over: a wave per packet (<= 4096),
+    16-packet k_seg chunks (< 65536) and 64-packet ones, all bit-exact."""
+    import rxgen
+    for npk, want in ((4096, "k_loop"), (4097, "c16"), (65535, "c16"), (65536, "k_seg")):
+        name = batch.ragged_variant(mode, npk)
+        assert name.startswith(want) or want in name, (npk, name)
+        if npk == 65536:
+            assert "c16" not in name
+        rng = np.random.default_rng(npk + mode)
+        if mode == O.MODE_VERIFY_RX:
+            blob, offs = rxgen.rx_batch(rng, npk, lo=0, hi=300)
+        else:
+            lens = rng.integers(20 if mode == O.MODE_VERIFY_TCP else 8, 400, size=npk)
+            blob, offs = _ragged(rng, lens, base_off=1)
+            if mode == O.MODE_VERIFY_TCP:
+                blob[offs[:-1].astype(np.int64) + 12] = 0x50
+        addrs = _rand(rng, 8 * npk) if mode in (O.MODE_UDP, O.MODE_VERIFY_TCP) else None
+        got = batch.checksum_ragged(_to(dev, blob), _to(dev, offs.view(np.int64)), mode,
+                                    addrs=None if addrs is None else _to(dev, addrs)).cpu().numpy()
+        want_v = oracle_c.batch(blob, mode, offsets=offs, addrs=addrs, threads=8)
+        assert np.array_equal(got, want_v), (mode, npk, np.nonzero(got != want_v)[0][:8])

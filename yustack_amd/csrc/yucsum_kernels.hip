@@ -1290,20 +1290,26 @@ struct SegChunk {
 // Loads only: the packet bounds and side data of the chunk starting at
 // packet p0. Ragged: offsets[]; uniform: i*stride (packets may leave gaps,
 // which are streamed but belong to no packet, or overlap).
+// A chunk is CH packets, lane l < CH owning packet p0 + l; lanes past the
+// chunk (l >= CH) or the batch sit at the chunk's end, so lane 63 always
+// holds it.
+template <int CH>
 __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
                                          uint64_t p0, uint32_t lane, SegChunk &k) {
   const uint64_t n = A.n;
   const uint64_t i = p0 + lane;
+  const uint64_t ce = p0 < n ? (n - p0 < (uint64_t)CH ? n : p0 + CH) : n;  // chunk end (packets)
+  const bool own = lane < (uint32_t)CH && i < n;
   // ragged: two (clamped) offset loads; uniform: arithmetic, with lanes past
-  // the batch at the chunk's end (its last packet's end)
-  const uint64_t last = p0 < n ? (n - p0 < 64u ? n : p0 + 64u) - 1u : 0u;
-  const uint64_t uy = (i < n ? i : last) * A.stride + A.len;
+  // the chunk at its end (its last packet's end)
+  const uint64_t last = p0 < n ? ce - 1u : 0u;
+  const uint64_t uy = (own ? i : last) * A.stride + A.len;
   const uint64_t *offs = A.offsets ? A.offsets : (const uint64_t *)g_side_zero;
-  const uint64_t ry = offs[A.offsets ? (i + 1 < n ? i + 1 : n) : 0];
-  const uint64_t rx = offs[A.offsets ? (i < n ? i : n) : 0];
-  k.ox = A.offsets ? rx : (i < n ? i * A.stride : uy);
+  const uint64_t ry = offs[A.offsets ? (own ? i + 1 : ce) : 0];
+  const uint64_t rx = offs[A.offsets ? (own ? i : ce) : 0];
+  k.ox = A.offsets ? rx : (own ? i * A.stride : uy);
   k.oy = A.offsets ? ry : uy;
-  k.sd = load_side(sp, i < n ? i : n - 1);  // b0/xe: seg_geom
+  k.sd = load_side(sp, own ? i : n - 1);  // b0/xe: seg_geom
 }
 
 
@@ -1431,7 +1437,7 @@ __device__ __forceinline__ uint64_t seg_waves(const BatchArgs &A) {
 // two ends), RX (VERIFY_RX: + header and transport ends).
 constexpr int kSegPlain = 0, kSegTx = 1, kSegRx = 2;
 
-template <int U, int NT, int K>
+template <int U, int NT, int K, int CH = 64>
 __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   constexpr bool RX = K == kSegRx;
   constexpr int NP = K == kSegPlain ? 2 : 4;  // point slots in use
@@ -1454,11 +1460,11 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   constexpr uint64_t kNoPt = ~0ull;          // a point slot not in use
 
   uint64_t ch = wave;
-  if (wave >= nwave || ch * 64u >= A.n) return;
+  if (wave >= nwave || ch * CH >= A.n) return;
   SegChunk cur, nxt;
-  seg_load(A, sp, ch * 64u, lane, cur);
-  seg_load(A, sp, (ch + nwave) * 64u, lane, nxt);
-  seg_geom(data, A.n, ch * 64u, cur);
+  seg_load<CH>(A, sp, ch * CH, lane, cur);
+  seg_load<CH>(A, sp, (ch + nwave) * CH, lane, nxt);
+  seg_geom(data, A.n, ch * CH, cur);
 
   // per-chunk state
   SegPt pt[4];  // start, end, then field start/end (TX) or header/transport end (RX)
@@ -1501,8 +1507,8 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
     SegChunk nn;  // the chunk after next: its loads go out before this
                   // step's tile loads, so waiting on them never waits on those
     if (last) {
-      seg_geom(data, A.n, (ch + nwave) * 64u, nxt);
-      seg_load(A, sp, (ch + 2u * nwave) * 64u, lane, nn);
+      seg_geom(data, A.n, (ch + nwave) * CH, nxt);
+      seg_load<CH>(A, sp, (ch + 2u * nwave) * CH, lane, nn);
     }
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
                           end, cn);
@@ -1603,8 +1609,8 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
     const bool own_end = !contig || lane == 63u;
     const uint32_t pe = own_end ? pt[1].p : nx_p;
     const uint32_t te = own_end ? pt[1].t : nx_t;
-    const uint64_t p = ch * 64u + lane;
-    if (p < A.n) {
+    const uint64_t p = ch * CH + lane;
+    if (lane < (uint32_t)CH && p < A.n) {
       const uint32_t odd = (uint32_t)pt[0].x & 1u;
       if (RX) {
         // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
@@ -1635,7 +1641,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
                       (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
       }
     }
-    if ((ch + nwave) * 64u >= A.n) return true;
+    if ((ch + nwave) * CH >= A.n) return true;
     cur = nxt;
     nxt = nn;
     ch += nwave;
@@ -1788,12 +1794,18 @@ const Variant kRag = {"k_rag<16,6>", 1536, {k_rag<16, 6, 0>, k_rag<16, 6, 1>, k_
 const Variant kHdr = {"k_hdr", 0, {k_hdr<0>, k_hdr<1>, k_hdr<0>}, 64, 64};
 #define YU_SEG(U, K, name) \
   {name, 0, {k_seg<U, 0, K>, k_seg<U, 1, K>, k_seg<U, 1, K>}, 64, 64}
+#define YU_SEG16(U, K, name) \
+  {name, 0, {k_seg<U, 0, K, 16>, k_seg<U, 1, K, 16>, k_seg<U, 1, K, 16>}, 64, 16}
 const Variant kSeg4 = YU_SEG(4, kSegPlain, "k_seg<4>");
 const Variant kSeg8 = YU_SEG(8, kSegPlain, "k_seg<8>");
 const Variant kSegTx4 = YU_SEG(4, kSegTx, "k_seg<4,tx>");
 const Variant kSegTx8 = YU_SEG(8, kSegTx, "k_seg<8,tx>");
 const Variant kSegRx4 = YU_SEG(4, kSegRx, "k_seg<4,rx>");
 const Variant kSegRx8 = YU_SEG(8, kSegRx, "k_seg<8,rx>");
+// 16-packet chunks: 4x the waves for mid-size ragged batches (see pick_ragged)
+const Variant kSeg8c16 = YU_SEG16(8, kSegPlain, "k_seg<8,c16>");
+const Variant kSegTx8c16 = YU_SEG16(8, kSegTx, "k_seg<8,tx,c16>");
+const Variant kSegRx8c16 = YU_SEG16(8, kSegRx, "k_seg<8,rx,c16>");
 
 // The k_seg kind for a mode (not the IPv4 header-only modes).
 const Variant &seg_for(bool u8, int mode) {
@@ -1817,6 +1829,7 @@ const Variant &seg_for(bool u8, int mode) {
 // from 16384 packets on k_seg wins on small packets (5.4 vs 11.5). VERIFY_RX
 // bursts take k_loop_rx, the same shape.
 constexpr uint64_t kSmallBurst = 4096;
+constexpr uint64_t kMidBatch = 65536;
 
 const Variant &pick_ragged(int mode, uint64_t n) {
   static const char *f = getenv("YU_RAGGED");
@@ -1826,7 +1839,13 @@ const Variant &pick_ragged(int mode, uint64_t n) {
   if (f && strcmp(f, "loop") == 0) return loop;
   if (f && strcmp(f, "rag") == 0 && !rx) return kRag;
   if (mode_is_ipv4(mode)) return kHdr;  // header-only: one lane per packet
+  if (f && strcmp(f, "seg16") == 0) return rx ? kSegRx8c16 : (mode_is_tx(mode) ? kSegTx8c16 : kSeg8c16);
   if (n <= kSmallBurst && !f) return loop;
+  // up to 64K packets: 16-packet chunks, 4x the waves (U{64..1500}: 8192
+  // packets 11.2 -> 6.3 us, 32768 11.7 -> 8.7; U{40..200} 5.1 -> 4.4; jumbo
+  // 44.2 -> 17.0; VERIFY_RX 13.3 -> 7.1); from 65536 on 64-packet chunks win
+  // again (13.1 vs 14.7 us; profiles/r01/kbench_kseg_chunk16_sweep.log)
+  if (n < kMidBatch && !f) return rx ? kSegRx8c16 : (mode_is_tx(mode) ? kSegTx8c16 : kSeg8c16);
   return seg_for(!seg4, mode);
 }
 
