@@ -58,10 +58,10 @@
 //     sparse ones). A wave holds 64/G packets per step; each group of G lanes
 //     loads its packet window in U dwordx4 loads per lane, reduces with log2(G)
 //     DPP adds and its last lane finishes the packet (config 3: k_small<16,6>).
-//   k_seg<U, NT, K>: ragged batches of more than 4096 packets, VERIFY_RX, and
-//     dense uniform packets of other sizes: a segmented sum over the byte
-//     stream of 64 consecutive packets per wave, U KiB tiles, packet sums as
-//     prefix differences (config 4, tun RX).
+//   k_seg<U, NT, K, CH>: ragged batches of more than 4096 packets, VERIFY_RX,
+//     and dense uniform packets of other sizes: a segmented sum over the byte
+//     stream of CH consecutive packets per wave (64, or 16 below 64K packets),
+//     U KiB tiles, packet sums as prefix differences (config 4, tun RX).
 //   k_hdr<NT>: the IPv4 header-only modes (<= 60 bytes of each packet), uniform
 //     and ragged: one lane per packet, 32-byte reads.
 //   k_loop<U, BE> / k_loop_rx<U>: one wave per packet, for ragged bursts of up
