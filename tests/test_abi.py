@@ -159,8 +159,9 @@ def test_python_front_end_refuses_cpu_tensors():
     (1500, 1500, "tcp", 0, "k_small<16,6>"),
     (1500, 1500, "tcp", 2, "k_small<16,6>"),     # 1503 still fits 1536
     (1536, 1536, "raw", 1, "k_small<32,4>"),     # 1539 > 1536
-    (9000, 9000, "raw", 0, "k_loop<4,LE>"),      # few packets (n = 1 here): a wave per packet
-    (200000, 200000, "raw", 0, "k_loop<4,BE>"),  # > 131072: exact uint32 wrap path
+    (9000, 9000, "raw", 0, "k_seg<8>"),          # dense > 3 KiB in a large batch
+    (20000, 9000, "raw", 0, "k_loop<4,LE>"),     # sparse: a wave per packet
+    (400000, 200000, "raw", 0, "k_loop<4,BE>"),  # sparse, > 131072: exact uint32 wrap path
     (1500, 1500, "ipv4", 0, "k_hdr"),            # only the <= 60-byte header is read
     (20, 20, "udp", 3, "k_seg<4,tx>"),
     (320, 320, "tcp", 0, "k_seg<4,tx>"),        # 129..704 B dense
@@ -169,12 +170,15 @@ def test_python_front_end_refuses_cpu_tensors():
     (200, 62, "raw", 1, "k_small<8,1>"),     # sparse: 65 > 64
 ])
 def test_variant_selection(stride, length, mode, align, want):
-    assert batch.variant(stride, length, mode, align) == want
+    assert batch.variant(stride, length, mode, align, n=1 << 20) == want
 
 
 @pytest.mark.parametrize("stride,length,n,want", [
     (9000, 9000, 1 << 20, "k_seg<8>"),      # dense > 3 KiB, enough chunks for the GPU
     (9000, 9000, 1000, "k_loop<4,LE>"),     # a few huge packets: a wave per packet
+    (320, 320, 1000, "k_small<16,2>"),       # small batches keep per-packet lane groups
+    (320, 320, 1 << 20, "k_seg<4>"),
+    (66, 66, 1000, "k_small<8,1>"),          # unaligned, small batch
     (200000, 200000, 1 << 17, "k_seg<8>"),  # > 131072: k_seg's exact byte-sum path
     (20000, 9000, 1 << 20, "k_loop<4,LE>"),  # sparse
 ])

@@ -802,7 +802,7 @@ def test_random_batches_fuzz(dev, oracle_c):
             want = oracle_c.batch(blob[align:], mode, stride=stride, length=length, n=n,
                                   initial_arr=init, initial=initial, addrs=addrs)
             d = _to(dev, blob)
-            seen.add(batch.variant(stride, length, mode, align))
+            seen.add(batch.variant(stride, length, mode, align, n=n))
             got = batch.checksum_uniform(d[align:], stride, length, n, mode, initial=initial,
                                          initial_arr=None if init is None else _to(dev, init),
                                          addrs=None if addrs is None else _to(dev, addrs),
@@ -888,15 +888,18 @@ def test_host_fill_paths(dev, oracle_c):
 
 
 def test_uniform_large_dense_batches_take_k_seg(dev, oracle_c):
-    """Dense uniform packets above 3 KiB in a large batch run on k_seg (8 KiB
-    tiles): parity for TCP segments and RAW packets with a per-packet initial."""
+    """Dense uniform packets in a large batch that go to k_seg (above 3 KiB, 129..704
+    bytes, or not 4-aligned): parity for TCP / UDP / RAW / VERIFY_UDP."""
     rng = np.random.default_rng(31)
-    for L, mode, n in ((4100, O.MODE_TCP, 70_000), (9001, O.MODE_RAW, 65_536)):
-        assert batch.variant(L, L, mode, 0, n=n) == ("k_seg<8,tx>" if mode == O.MODE_TCP else "k_seg<8>")
+    cases = ((4100, O.MODE_TCP, 70_000, "k_seg<8,tx>"), (9001, O.MODE_RAW, 65_536, "k_seg<8>"),
+             (300, O.MODE_TCP, 70_000, "k_seg<4,tx>"), (66, O.MODE_UDP, 70_000, "k_seg<4,tx>"),
+             (500, O.MODE_VERIFY_UDP, 65_536, "k_seg<8>"))
+    for L, mode, n, want_kernel in cases:
+        assert batch.variant(L, L, mode, 0, n=n) == want_kernel
         host = _rand(rng, n * L)
         if mode == O.MODE_TCP:
             host[12::L] = 0x50
-        addrs = _rand(rng, 8 * n) if mode == O.MODE_TCP else None
+        addrs = _rand(rng, 8 * n) if mode in (O.MODE_TCP, O.MODE_UDP, O.MODE_VERIFY_UDP) else None
         init = rng.integers(0, 65536, size=n, dtype=np.uint16) if mode == O.MODE_RAW else None
         got = batch.checksum_uniform(_to(dev, host), L, L, n, mode,
                                      addrs=None if addrs is None else _to(dev, addrs),

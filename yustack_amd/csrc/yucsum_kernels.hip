@@ -1904,13 +1904,15 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
   // 320: 58-66 vs 88-89; 512: 87 vs 103; 704: 116 vs 120; unaligned 66 B: 26.8
   // vs 38.6; from 768 on k_small is as fast or faster; tools/kbench 14,
   // profiles/r01/kbench_uniform_size_sweep.log)
-  const bool dense = 2u * stride <= 3u * (uint64_t)len;
+  // (k_seg gives one wave to 64 packets: only batches of 64K packets or more
+  // have enough of them to fill the GPU; smaller ones keep the per-packet shapes)
+  const bool dense = 2u * stride <= 3u * (uint64_t)len && n >= kMidBatch;
   if (len <= 704u && dense) return seg_for(len >= 448u, mode);
   // and above 3 KiB, where it streams 8 KiB tiles past k_small<64,4> and the
   // one-wave-per-packet k_loop (4096 B: 636 vs 664 us; 9000 B: 1373 vs 1464;
   // 16 KiB: 0.88 vs 0.81 of peak) — given enough 64-packet chunks to fill the
   // GPU (one wave each); a few huge packets keep k_loop's wave per packet
-  if (len > 3072u && dense && n >= 65536u) return seg_for(true, mode);
+  if (len > 3072u && dense) return seg_for(true, mode);
   for (const Variant &v : kSmall)
     if (fits(v)) return v;
   return len > kLEMax ? kLoopBE : kLoopLE;
