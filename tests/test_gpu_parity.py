@@ -761,13 +761,19 @@ def test_random_batches_fuzz(dev, oracle_c):
     selection can pick (k_tiny, k_lane, k_small, k_hdr, k_seg, k_loop), against the
     C oracle on the same bytes. Seeded, so a failure reproduces."""
     import os
-    # YU_FUZZ_SEED / YU_FUZZ_ITERS: longer or different runs by hand
+    # YU_FUZZ_SEED / YU_FUZZ_ITERS: longer or different runs by hand; YU_FUZZ_NBIG
+    # raises the largest batch size drawn (default 6000; 70000 reaches the 16-packet
+    # k_seg chunks of ragged batches up to 65535 and the uniform k_seg choice at 64K)
     rng = np.random.default_rng(int(os.environ.get("YU_FUZZ_SEED", "2026")))
+    nbig = int(os.environ.get("YU_FUZZ_NBIG", "6000"))
+    iters = int(os.environ.get("YU_FUZZ_ITERS", "800"))
     seen = set()
-    for it in range(int(os.environ.get("YU_FUZZ_ITERS", "800"))):
+    for it in range(iters):
+        if iters > 800 and it % 100 == 0:
+            print(f"fuzz {it}/{iters} variants so far: {sorted(seen)}", flush=True)
         mode = int(rng.integers(0, 8))  # VERIFY_RX has its own tests (real headers)
         lo = _MIN_LEN.get(mode, 0)
-        n = int(rng.choice([1, 2, 63, 64, 65, int(rng.integers(1, 3000)), int(rng.integers(4097, 6000))]))
+        n = int(rng.choice([1, 2, 63, 64, 65, int(rng.integers(1, 3000)), int(rng.integers(4097, nbig))]))
         ragged = bool(rng.integers(0, 2))
         side = int(rng.integers(0, 3))  # 0: scalar initial, 1: initial_arr, 2: addrs
         tx = mode in _FIELD or mode == O.MODE_IPV4
