@@ -233,6 +233,32 @@ def test_verify_rx_ragged(dev, oracle_c, lo, hi, npk):
     assert len(np.unique(want)) >= 5
 
 
+def test_verify_rx_fuzz(dev, oracle_c):
+    """Seeded RX batches whose sizes straddle every VERIFY_RX kernel cut-over (a wave
+    per datagram up to 4096, 16-datagram k_seg chunks up to 65535, 64-datagram chunks
+    from 65536): verification bits against the oracle at a random start alignment.
+    YU_RX_FUZZ_SEED / YU_RX_FUZZ_ITERS for longer runs by hand."""
+    import os
+    import rxgen
+    rng = np.random.default_rng(int(os.environ.get("YU_RX_FUZZ_SEED", "4242")))
+    seen = set()
+    sizes = [1, 2, 63, 64, 65, 4096, 4097, 65535, 65536, 70000]
+    for it in range(int(os.environ.get("YU_RX_FUZZ_ITERS", "12"))):
+        npk = sizes[it] if it < len(sizes) else int(rng.integers(1, 20000))
+        lo, hi = [(0, 40), (0, 300), (0, 1480), (1000, 9000)][int(rng.integers(0, 4))]
+        if npk > 10000:
+            lo, hi = min(lo, 100), min(hi, 300)  # keeps the Python packet generator to seconds
+        blob, offs = rxgen.rx_batch(rng, npk, lo=lo, hi=hi, bad=float(rng.random()))
+        base_off = int(rng.integers(0, 16))
+        b = np.concatenate([np.zeros(base_off, np.uint8), blob, np.zeros(32, np.uint8)])
+        o = offs + base_off
+        seen.add(batch.ragged_variant("verify_rx", npk))
+        got = batch.checksum_ragged(_to(dev, b), _to(dev, o.view(np.int64)), "verify_rx").cpu().numpy()
+        want = oracle_c.batch(b, O.MODE_VERIFY_RX, offsets=o)
+        assert np.array_equal(got, want), (it, npk, lo, hi, base_off, np.nonzero(got != want)[0][:10])
+    assert {"k_loop<4,rx>", "k_seg<8,rx,c16>", "k_seg<8,rx>"} <= seen, seen
+
+
 @pytest.mark.parametrize("npk", [777, 5000])
 @pytest.mark.parametrize("length", [20, 40, 64, 576, 1500])
 def test_verify_rx_uniform(dev, oracle_c, length, npk):
