@@ -106,28 +106,36 @@ func BatchHostUniform(data []byte, stride uint64, length uint32, n uint64, mode 
 	if n == 0 {
 		return nil
 	}
-	if uint64(len(out)) < n || uint64(len(data)) < (n-1)*stride+uint64(length) {
-		return fmt.Errorf("checksum: batch buffers too small")
+	// overflow-safe form of (n-1)*stride+length <= len(data)
+	if uint64(len(out)) < n || uint64(length) > uint64(len(data)) ||
+		(n > 1 && stride > (uint64(len(data))-uint64(length))/(n-1)) {
+		return errTooSmall
 	}
-	var pi *C.uint16_t
-	if initial != nil {
-		pi = (*C.uint16_t)(unsafe.Pointer(&initial[0]))
+	if err := checkSide(n, initial, addrs); err != nil {
+		return err
 	}
-	var pa *C.uint8_t
-	if addrs != nil {
-		pa = (*C.uint8_t)(unsafe.Pointer(&addrs[0]))
+	var pd *C.uint8_t
+	if len(data) > 0 {
+		pd = (*C.uint8_t)(unsafe.Pointer(&data[0]))
 	}
-	rc := C.yu_csum_batch_host_uniform((*C.uint8_t)(unsafe.Pointer(&data[0])), C.uint64_t(stride),
+	pi, pa := sideArgs(initial, addrs)
+	return status(C.yu_csum_batch_host_uniform(pd, C.uint64_t(stride),
 		C.uint32_t(length), C.uint64_t(n), C.int(mode), pi, 0, pa,
-		(*C.uint16_t)(unsafe.Pointer(&out[0])), C.int(device))
-	switch {
-	case rc == C.YU_OK:
-		return nil
-	case rc == C.YU_ENODEV:
-		return ErrNoDevice
-	default:
-		return fmt.Errorf("checksum: %s (%d)", C.GoString(C.yu_strerror(rc)), int(rc))
+		(*C.uint16_t)(unsafe.Pointer(&out[0])), C.int(device)))
+}
+
+var errTooSmall = errors.New("checksum: batch buffers too small")
+
+// checkSide rejects optional side arrays shorter than the batch: the C calls
+// read n initial values (2n bytes) and n address records (8n bytes).
+func checkSide(n uint64, initial []uint16, addrs []byte) error {
+	if len(initial) > 0 && uint64(len(initial)) < n {
+		return fmt.Errorf("checksum: initial has %d values for %d packets", len(initial), n)
 	}
+	if len(addrs) > 0 && (n > uint64(len(addrs))/8) {
+		return fmt.Errorf("checksum: addrs has %d bytes for %d packets (8 each)", len(addrs), n)
+	}
+	return nil
 }
 
 func status(rc C.int) error {
@@ -178,7 +186,10 @@ func BatchHostRagged(data []byte, offsets []uint64, mode Mode, initial []uint16,
 	}
 	n := uint64(len(offsets) - 1)
 	if uint64(len(out)) < n || offsets[n] > uint64(len(data)) {
-		return fmt.Errorf("checksum: batch buffers too small")
+		return errTooSmall
+	}
+	if err := checkSide(n, initial, addrs); err != nil {
+		return err
 	}
 	var pd *C.uint8_t
 	if len(data) > 0 {
@@ -199,7 +210,10 @@ func BatchHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, 
 		return nil
 	}
 	if len(out) < len(pkts) {
-		return fmt.Errorf("checksum: batch buffers too small")
+		return errTooSmall
+	}
+	if err := checkSide(uint64(len(pkts)), initial, addrs); err != nil {
+		return err
 	}
 	pi, pa := sideArgs(initial, addrs)
 	d, nd := deviceList(devices)
@@ -223,9 +237,12 @@ func FillHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, o
 	var po *C.uint16_t
 	if out != nil {
 		if len(out) < len(pkts) {
-			return fmt.Errorf("checksum: batch buffers too small")
+			return errTooSmall
 		}
 		po = (*C.uint16_t)(unsafe.Pointer(&out[0]))
+	}
+	if err := checkSide(uint64(len(pkts)), initial, addrs); err != nil {
+		return err
 	}
 	pi, pa := sideArgs(initial, addrs)
 	return withPackets(pkts, func(iov *C.yu_iovec, first *C.uint64_t, n C.uint64_t) C.int {

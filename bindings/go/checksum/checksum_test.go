@@ -120,3 +120,34 @@ func TestFillHostPackets(t *testing.T) {
 		}
 	}
 }
+
+// TestShortArgumentsRejected: too-short side arrays and a data slice that a
+// wrapping size product would let through are errors, never reads past the Go
+// allocation (no device needed: the checks run before any C call).
+func TestShortArgumentsRejected(t *testing.T) {
+	data := make([]byte, 4*100)
+	out := make([]uint16, 4)
+	if BatchHostUniform(data, 100, 100, 4, ModeRaw, make([]uint16, 3), nil, out, 0) == nil {
+		t.Fatal("initial shorter than n accepted")
+	}
+	if BatchHostUniform(data, 100, 100, 4, ModeUDP, nil, make([]byte, 31), out, 0) == nil {
+		t.Fatal("addrs shorter than 8n accepted")
+	}
+	if BatchHostUniform(data, 1<<63, 100, 3, ModeRaw, nil, nil, out, 0) == nil {
+		t.Fatal("wrapping (n-1)*stride accepted")
+	}
+	if BatchHostUniform(data, 100, 500, 1, ModeRaw, nil, nil, out, 0) == nil {
+		t.Fatal("length past data accepted")
+	}
+	offs := []uint64{0, 100, 200, 300, 400}
+	if BatchHostRagged(data, offs, ModeRaw, make([]uint16, 2), nil, out) == nil {
+		t.Fatal("ragged: short initial accepted")
+	}
+	pkts := [][]byte{data[:100], data[100:200]}
+	if BatchHostPackets(pkts, ModeUDP, nil, make([]byte, 8), out) == nil {
+		t.Fatal("packets: short addrs accepted")
+	}
+	if FillHostPackets(pkts, ModeUDP, make([]uint16, 1), nil, nil, 0) == nil {
+		t.Fatal("fill: short initial accepted")
+	}
+}

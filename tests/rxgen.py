@@ -88,3 +88,73 @@ def rx_batch(rng, n, lo=0, hi=1480, bad=0.5):
     offs = np.zeros(n + 1, np.uint64)
     offs[1:] = np.cumsum([len(p) for p in pkts])
     return np.frombuffer(b"".join(pkts), dtype=np.uint8).copy(), offs
+
+
+def short_header_packet(rng, total):
+    """A received datagram of `total` >= 20 bytes whose IPv4 header length is under
+    20 bytes (IHL 0..4, which IsValid accepts: header/ipv4.go:126-138), with a total
+    length that is often under 20 too, so the header and transport end points both
+    fall inside the first 20 bytes. Some have an IP sum that checks (IHL 0, or IHL
+    >= 2 with the ID field set to make the sum 0xFFFF), some an ICMP payload that
+    is empty (transport sum 0), some a total length past the packet (invalid)."""
+    pkt = bytearray(rng.integers(0, 256, size=total, dtype=np.uint8).tobytes())
+    ihl = int(rng.integers(0, 5))
+    hl = 4 * ihl
+    r = rng.random()
+    if r < 0.3:
+        tl = hl
+    elif r < 0.7:
+        tl = int(rng.integers(hl, 20))
+    elif r < 0.9:
+        tl = int(rng.integers(hl, total + 1))
+    else:
+        tl = total + int(rng.integers(1, 50))  # IsValid: tl > pktSize
+    pkt[0] = 0x40 | ihl
+    _fill16(pkt, 2, tl)
+    pkt[9] = int(rng.choice([6, 17, 1, 47]))
+    if hl >= 8 and rng.random() < 0.5:  # ID field chosen so the header sums to 0xFFFF
+        pkt[4] = pkt[5] = 0
+        _fill16(pkt, 4, (0xFFFF - O.checksum(bytes(pkt[:hl]), 0)) & 0xFFFF)
+    return pkt
+
+
+def filler_packet(rng, total):
+    """A `total`-byte datagram with a plain IHL-5 header (tl = total, random
+    protocol) and unfixed checksums: it only moves the next packet's start."""
+    pkt = bytearray(rng.integers(0, 256, size=total, dtype=np.uint8).tobytes())
+    if total >= 20:
+        pkt[0] = 0x45
+        _fill16(pkt, 2, total)
+        pkt[9] = int(rng.choice([6, 17, 1, 47]))
+    return pkt
+
+
+def tile_edge_batch(rng, n, chunk, base_off, tile=4096):
+    """Ragged RX batch whose short-header packets (short_header_packet) start so that
+    floor4(start) lies 4..20 bytes before a tile boundary of k_seg's chunk-relative
+    tiling (b0 = floor4 of the chunk's first start; boundaries every `tile` bytes,
+    both the 4 KiB and the 8 KiB ones). Each is preceded by a filler sized to put
+    it there. Returns (blob incl. base_off leading bytes + 32 slack, offsets)."""
+    pkts, offs = [], [base_off]
+    pos = base_off
+    b0 = 0
+    special_next = False
+    for i in range(n):
+        if i % chunk == 0:
+            b0 = pos & ~3
+        if special_next:
+            p = short_header_packet(rng, int(rng.integers(20, 81)))
+            special_next = False
+        else:
+            d = 4 * int(rng.integers(1, 6))
+            s = int(rng.integers(0, 4))
+            m = -(-(pos + 40 - b0) // tile)  # first boundary leaving a >= 20-byte filler
+            start = b0 + m * tile - d + s
+            p = filler_packet(rng, start - pos)
+            special_next = (i + 1) % chunk != 0  # the next packet stays in this chunk
+        pkts.append(bytes(p))
+        pos += len(p)
+        offs.append(pos)
+    blob = np.zeros(pos + 32, np.uint8)
+    blob[base_off:pos] = np.frombuffer(b"".join(pkts), np.uint8)
+    return blob, np.array(offs, np.uint64)

@@ -46,3 +46,28 @@ def test_cgo_preamble_compiles_as_c(tmp_path):
     r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only",
                         f"-I{ROOT}/include", str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def _func_body(go, name):
+    m = re.search(rf"\nfunc {name}\(.*?\n}}\n", go, re.S)
+    assert m, name
+    return m.group(0)
+
+
+def test_go_batch_calls_check_side_arrays_and_sizes():
+    """Every Go batch entry point rejects initial / addrs slices shorter than the
+    batch before the C call reads 2n / 8n bytes of them, passes side arrays only
+    through sideArgs (no &initial[0] on an empty slice), and BatchHostUniform's data
+    size check cannot wrap."""
+    go = _go()
+    side = _func_body(go, "checkSide")
+    assert "uint64(len(initial)) < n" in side and "uint64(len(addrs))/8" in side
+    for f in ("BatchHostUniform", "BatchHostRagged", "BatchHostPackets", "FillHostPackets"):
+        body = _func_body(go, f)
+        assert "checkSide(" in body, f
+        assert "sideArgs(initial, addrs)" in body, f
+        assert body.index("checkSide(") < body.index("C.yu_") if "C.yu_" in body else True, f
+        assert "&initial[0]" not in body and "&addrs[0]" not in body, f
+    uni = _func_body(go, "BatchHostUniform")
+    assert "(n-1)*stride" not in uni.replace("// overflow-safe form of (n-1)*stride", "")
+    assert "/(n-1)" in uni

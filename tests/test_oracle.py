@@ -121,6 +121,34 @@ def test_rx_twins_agree(oracle_c):
     assert set(np.unique(want).tolist()) >= {0, 1, 2, 3, 6, 7, 8}  # every outcome occurs
 
 
+def test_rx_tile_edge_generator(oracle_c):
+    """The data of test_verify_rx_header_straddles_tile: every short-header datagram
+    that is not its chunk's first has floor4(start) 4..20 bytes before a 4 KiB
+    boundary of its chunk's tiling (some before an 8 KiB one), IHL 0..4; the C and
+    Python oracles agree on it and every RX outcome occurs."""
+    import rxgen
+    rng = np.random.default_rng(5)
+    for chunk, base_off in ((16, 0), (64, 3)):
+        blob, offs = rxgen.tile_edge_batch(rng, 700, chunk, base_off)
+        n = len(offs) - 1
+        assert int(offs[0]) == base_off and np.all(np.diff(offs.astype(np.int64)) >= 20)
+        d8 = 0
+        for i in range(1, n, 2):
+            if i % chunk == 0:
+                continue
+            b0 = int(offs[i - i % chunk]) & ~3
+            rel = (int(offs[i]) & ~3) - b0
+            assert 4 <= (-rel) % 4096 <= 20, (i, rel)
+            d8 += 4 <= (-rel) % 8192 <= 20
+            assert blob[int(offs[i])] & 0xF < 5
+        assert d8 > 10
+        want = O.batch_ragged_py(blob.tobytes(), offs, O.MODE_VERIFY_RX)
+        got = oracle_c.batch(blob, O.MODE_VERIFY_RX, offsets=offs)
+        assert (got == want).all()
+        short = want[1::2]
+        assert set(np.unique(short).tolist()) >= {1, 2, 3, 6, 7, 8}
+
+
 def test_twins_agree_random(oracle_c):
     rng = random.Random(99)
     for _ in range(400):

@@ -1549,6 +1549,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
         s_pre[wid][u * 64 + lane] = pl[u];
       }
       __builtin_amdgcn_wave_barrier();
+      bool parsed = false;
       if (RX && rx.need) {  // gather header dwords held by this tile, parse
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
@@ -1563,6 +1564,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
           rx_parse(rx, (uint32_t)pt[0].x & 3u, cur.oy - cur.ox, hl, tl);
           pt[2].x = pt[0].x + hl;
           pt[3].x = pt[0].x + tl;
+          parsed = true;
         }
       }
 #pragma unroll
@@ -1571,6 +1573,25 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
         if (q < T) {
           const uint32_t k = (uint32_t)q >> 4;
           pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
+        }
+      }
+      if (RX && parsed) {
+        // A header straddling two tiles is parsed in the second, but a header
+        // or total length under 20 bytes (IsValid accepts IHL 0..4) can put
+        // its point in the first, whose bytes have gone by. Such a point lies
+        // inside the gathered 24-byte window: P(point) = P(start) + the LE sum
+        // of the window bytes in between, taken from the registers.
+        const uint32_t sh = (uint32_t)pt[0].x & 3u;
+#pragma unroll
+        for (int i = 2; i < 4; ++i) {
+          if (pt[i].x < tb) {
+            const uint32_t b = sh + (uint32_t)(pt[i].x - pt[0].x);  // < sh + 20
+            uint32_t s = pt[0].p;
+#pragma unroll
+            for (int j = 0; j < 6; ++j)
+              s = sad(rx.h[j] & byte_range_mask(4u * (uint32_t)j, sh, b), s);
+            pt[i].p = s;
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();
