@@ -99,6 +99,15 @@ def test_argument_validation_precedes_device():
     assert L.yu_csum_batch_uniform(p, 16, 4, 4, 1, None, 0, None, o, None) == _lib.YU_EINVAL  # < UDP header
     assert L.yu_csum_batch_uniform(p, 16, 0xFFFF0001, 1, 0, None, 0, None, o, None) == _lib.YU_EINVAL  # > YU_MAX_RAW_LEN
     assert L.yu_csum_batch_uniform(p, 16, 16, 0, 0, None, 0, None, o, None) == 0  # empty batch: no-op
+    # (n-1)*stride + len past the end of the address space: rejected, not wrapped
+    huge = 1 << 62
+    assert L.yu_csum_batch_uniform(p, huge, 16, 5, 0, None, 0, None, o, None) == _lib.YU_EINVAL
+    assert L.yu_csum_fill_uniform(p, huge, 16, 5, 1, None, 0, None, o, None) == _lib.YU_EINVAL
+    assert L.yu_csum_batch_host_uniform(p, huge, 16, 5, 0, None, 0, None, o, 0) == _lib.YU_EINVAL
+    assert L.yu_csum_fill_host_uniform(p, huge, 16, 5, 1, None, 0, None, o, 0) == _lib.YU_EINVAL
+    devs1 = (ctypes.c_int * 1)(0)
+    assert L.yu_csum_batch_host_uniform_multi(p, huge, 16, 5, 0, None, 0, None, o, ctypes.addressof(devs1),
+                                              1) == _lib.YU_EINVAL
     assert L.yu_csum_fill_uniform(p, 16, 16, 4, 0, None, 0, None, o, None) == _lib.YU_EINVAL  # RAW not TX
     assert L.yu_csum_fill_uniform(p + 1, 16, 16, 4, 1, None, 0, None, o, None) == _lib.YU_EINVAL  # unaligned
     assert L.yu_csum_batch_ragged(p, None, 4, 0, None, 0, None, o, None) == _lib.YU_EINVAL

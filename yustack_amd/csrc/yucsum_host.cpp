@@ -340,6 +340,10 @@ int direct(Slot &x, const Layout &L, uint64_t n, const uint16_t *h_init,
 // span, how to stage them (returning the host pointer the H2D copy reads:
 // the caller's pinned buffer or the slot's staging), and how to launch.
 template <class Layout>
+int run_slices(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
+               const uint8_t *h_addrs, uint16_t *h_out, bool pin_out);
+
+template <class Layout>
 int pipeline(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
              const uint8_t *h_addrs, uint16_t *h_out) {
   // capacity: the largest slice of this batch
@@ -353,11 +357,27 @@ int pipeline(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
   }
   int rc = c.reserve(max_b, max_pk);
   if (rc) return rc;
-  if (max_pk == n && max_b <= direct_max()) {
-    rc = direct(c.s[0], L, n, h_init, h_addrs, h_out);
-    if (rc != kNoDirect) return rc;
+  rc = kNoDirect;
+  if (max_pk == n && max_b <= direct_max()) rc = direct(c.s[0], L, n, h_init, h_addrs, h_out);
+  if (rc == kNoDirect) rc = run_slices(c, L, n, h_init, h_addrs, h_out, is_pinned(h_out));
+  if (rc) {
+    // A failed call returns with no transfer still aimed at the caller's
+    // buffers: every slot's stream is drained before the error goes back (a
+    // pinned input is read, and a pinned h_out written, by the copies
+    // themselves, including those of a slice that failed halfway).
+    for (Slot &x : c.s) {
+      if (x.st) (void)hipStreamSynchronize(x.st);
+      x.busy = false;
+    }
+    (void)hipGetLastError();
   }
-  const bool pin_out = is_pinned(h_out);
+  return rc;
+}
+
+template <class Layout>
+int run_slices(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
+               const uint8_t *h_addrs, uint16_t *h_out, bool pin_out) {
+  int rc = YU_OK;
   uint64_t k = 0;
   for (uint64_t first = 0; first < n; ++k) {
     Slot &x = c.s[k % kSlots];
@@ -539,6 +559,12 @@ int on_device(int device, F &&f) {
 
 bool bad_mode(int mode) { return mode < 0 || mode >= YU_MODE_COUNT; }
 
+// A uniform batch [data, data + (n-1)*stride + len) that would wrap the
+// address space (a nonsense stride or count) is rejected before any copy.
+bool span_wraps(const uint8_t *data, uint64_t stride, uint32_t len, uint64_t n) {
+  return n > 1 && stride > (UINT64_MAX - (uint64_t)(uintptr_t)data - len) / (n - 1);
+}
+
 // Host offsets are checked here, unlike the device call's: non-decreasing,
 // every packet within the mode's length limit.
 int check_offsets(const uint64_t *off, uint64_t n, int mode) {
@@ -681,6 +707,7 @@ extern "C" int yu_csum_batch_host_uniform(const uint8_t *h_data,
   if (!h_data && len) return YU_EINVAL;
   if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
   if (len > YU_MAX_RAW_LEN) return YU_EINVAL;
+  if (span_wraps(h_data, stride, len, n)) return YU_EINVAL;
   return on_device(device, [&](Ctx &c) {
     const uint64_t pstride = stride ? stride : 1;
     uint64_t slice = kSliceBytes / pstride;
@@ -733,6 +760,7 @@ extern "C" int yu_csum_batch_host_uniform_multi(const uint8_t *h_data, uint64_t 
   if (!h_data && len) return YU_EINVAL;
   if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
   if (len > YU_MAX_RAW_LEN) return YU_EINVAL;
+  if (span_wraps(h_data, stride, len, n)) return YU_EINVAL;
   if (int rc = check_devices(devices, ndev)) return rc;
   return fan_out(devices, ndev, even_bounds(n, ndev), [&](int i, uint64_t a, uint64_t cnt) {
     return yu_csum_batch_host_uniform(h_data ? h_data + a * stride : nullptr, stride, len, cnt,

@@ -2048,6 +2048,8 @@ int batch_uniform(const uint8_t *data, uint8_t *fill, uint64_t stride,
   if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
   if (len < min_len(mode)) return YU_EINVAL;
   if (len > YU_MAX_RAW_LEN) return YU_EINVAL;  // window offsets stay in uint32
+  // the batch [data, data + (n-1)*stride + len) must not wrap the address space
+  if (n > 1 && stride > (UINT64_MAX - (uint64_t)(uintptr_t)data - len) / (n - 1)) return YU_EINVAL;
   // fill: packets must start 4-byte aligned (no dword shared with a
   // neighbour's field)
   if (fill && (((uintptr_t)data | stride) & 3u)) return YU_EINVAL;
