@@ -358,6 +358,44 @@ def test_raw_uint32_wrap(dev, oracle_c):
     assert got[0] == 65534  # the reference's wrapped value (exact sum would give 65535)
 
 
+@pytest.mark.parametrize("L,pad", [(132, 0), (136, 0), (200, 4), (300, 0), (700, 0), (1500, 0), (1500, 8), (2000, 0),
+                                   (3000, 4), (4000, 0), (1500, 36)])
+@pytest.mark.parametrize("mode", [O.MODE_UDP, O.MODE_TCP, O.MODE_ICMP])
+def test_fill_k_small_every_alignment(dev, oracle_c, mode, L, pad):
+    """The in-place writer on every k_small shape it reaches (132..4000-byte packets,
+    dense and sparse): packets start at every 4-aligned offset mod 64 (device views
+    at base 0/4/36/60 plus the stride's steps); afterwards every byte but the fields
+    equals the input, first and last packet included, and the fields and results
+    equal the oracle's. (Written for a whole-64-byte-block writer that was measured
+    and rejected, profiles/r02/kbench_ab_fill_block64_rejected.log.)"""
+    rng = np.random.default_rng(5100 + 7 * L + pad + mode)
+    stride = L + pad
+    n = 777
+    rand = _rand(rng, n * stride + 64)
+    addrs = _rand(rng, 8 * n)
+    for base in (0, 4, 36, 60):
+        host = rand.copy()
+        if mode == O.MODE_TCP:  # DataOffset 5 (sendTCP's segments)
+            host[base + np.arange(n, dtype=np.int64) * stride + 12] = 0x50
+        assert batch.variant(stride, L, {1: "udp", 2: "tcp", 4: "icmp"}[mode], base, n=n).startswith("k_small<")
+        dfull = _to(dev, host)
+        assert dfull.data_ptr() % 64 == 0
+        d = dfull[base:]  # packets start at base mod 64 (plus the stride's steps)
+        a = _to(dev, addrs) if mode in (1, 2) else None
+        out = batch.checksum_uniform(d, stride, L, n, mode, addrs=a, fill=True).cpu().numpy()
+        want = oracle_c.batch(host[base:], mode, stride=stride, length=L, n=n,
+                              addrs=addrs if mode in (1, 2) else None)
+        assert np.array_equal(out, want), (base, np.nonzero(out != want)[0][:8])
+        got = dfull.cpu().numpy()
+        f = {O.MODE_UDP: 6, O.MODE_TCP: 16, O.MODE_ICMP: 2}[mode]
+        fidx = base + np.arange(n, dtype=np.int64) * stride + f
+        expect = host.copy()
+        expect[fidx] = (want >> 8).astype(np.uint8)
+        expect[fidx + 1] = (want & 0xFF).astype(np.uint8)
+        bad = np.nonzero(got != expect)[0]
+        assert bad.size == 0, (base, bad[:8])
+
+
 @pytest.mark.parametrize("L", [1500, 124, 100, 72, 64, 20])  # k_small / k_hdr, k_tiny<8>, k_lane<7,5,4,2>
 @pytest.mark.parametrize("mode", [O.MODE_UDP, O.MODE_TCP, O.MODE_IPV4, O.MODE_ICMP])
 def test_fill_in_place(dev, oracle_c, mode, L):
