@@ -726,6 +726,43 @@ def test_host_paths_concurrent_callers(dev, oracle_c):
 
 
 # ------------------------------------------------------------------ full-size properties
+@pytest.mark.parametrize("stride,length,mode,align,n,kern", [
+    (200, 40, "raw", 1, (1 << 18) + 7, "k_small<4,1>"),
+    (200, 60, "udp", 2, (1 << 18) + 7, "k_small<4,1>"),
+    (256, 70, "raw", 2, (1 << 18) + 7, "k_small<8,1>"),
+    (300, 136, "tcp", 0, (1 << 18) + 9, "k_small<8,2>"),
+    (1600, 1500, "udp", 0, (1 << 20) + 7, "k_small<16,6>"),
+    (2000, 2000, "raw", 0, (1 << 20) + 7, "k_small<32,4>"),
+])
+def test_k_small_runs_at_grid_size(dev, oracle_c, stride, length, mode, align, n, kern):
+    """k_small hands each wave 16 consecutive packets (one side-record load, one
+    result store per run) from 8 runs per CU up, and a wave takes further runs
+    grid-stride once the grid is full (CUs x blocks per CU x 4 waves; 16 blocks per
+    CU below G = 16 lanes per packet, 64 from there). These batches are past the
+    full grid, with a partial last run, at unaligned starts, with initial arrays
+    and address records; bit-exact against the oracle at full size. (Smaller
+    batches in the other tests cover the interleaved mapping below 8 runs per CU.)"""
+    mod = {"raw": O.MODE_RAW, "udp": O.MODE_UDP, "tcp": O.MODE_TCP}[mode]
+    assert batch.variant(stride, length, mode, align, n=n) == kern
+    G = int(kern.split("<")[1].split(",")[0])
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    assert n // 16 >= cus * (64 if G >= 16 else 16) * 4  # the run mapping applies
+    g = torch.Generator(device=dev)
+    g.manual_seed(n + stride)
+    total = align + (n - 1) * stride + length
+    d = torch.randint(0, 256, (total + 16,), dtype=torch.uint8, device=dev, generator=g)
+    if mode == "tcp":  # DataOffset 5
+        d[align + 12: align + 12 + (n - 1) * stride + 1: stride] = 0x50
+    ia = torch.randint(0, 1 << 16, (n,), dtype=torch.int32, device=dev, generator=g).to(torch.uint16) \
+        if mode == "raw" else None
+    ad = torch.randint(0, 256, (8 * n,), dtype=torch.uint8, device=dev, generator=g) if mode != "raw" else None
+    got = batch.checksum_uniform(d[align:], stride, length, n, mode, initial_arr=ia, addrs=ad).cpu().numpy()
+    want = oracle_c.batch(d.cpu().numpy()[align:], mod, stride=stride, length=length, n=n,
+                          initial_arr=None if ia is None else ia.cpu().numpy(),
+                          addrs=None if ad is None else ad.cpu().numpy(), threads=8)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
 def test_full_size_fill_then_verify_round_trip(dev):
     """Size-independent property at BASELINE config 3 and 4 sizes: writing the TX
     field in place (yu_csum_fill_*, SetChecksum semantics) and then verifying the same

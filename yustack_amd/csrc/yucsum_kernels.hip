@@ -372,13 +372,11 @@ __device__ __forceinline__ uint32_t packet_value(const BatchArgs &A, uint32_t v,
   return r;
 }
 
-__device__ __forceinline__ void finish_packet(const BatchArgs &A, uint64_t p,
-                                              uint32_t v, uint64_t len,
-                                              const Side &sd, uint8_t *pkt,
-                                              uint32_t hdr_end) {
+// The field value r stored big-endian into the packet (TX fill), if the
+// field lies inside the first hdr_end bytes.
+__device__ __forceinline__ void store_field(const BatchArgs &A, uint32_t r, uint8_t *pkt,
+                                            uint32_t hdr_end) {
   const int mode = A.mode;
-  const uint32_t r = packet_value(A, v, len, sd);
-  if (A.out) A.out[p] = (uint16_t)r;
   if (A.fill && mode_is_tx(mode)) {
     const uint32_t f = mode_field(mode);
     if (f + 2u <= hdr_end) {
@@ -398,6 +396,15 @@ __device__ __forceinline__ void finish_packet(const BatchArgs &A, uint64_t p,
       }
     }
   }
+}
+
+__device__ __forceinline__ void finish_packet(const BatchArgs &A, uint64_t p,
+                                              uint32_t v, uint64_t len,
+                                              const Side &sd, uint8_t *pkt,
+                                              uint32_t hdr_end) {
+  const uint32_t r = packet_value(A, v, len, sd);
+  if (A.out) A.out[p] = (uint16_t)r;
+  store_field(A, r, pkt, hdr_end);
 }
 
 // Chunk c at window offset cr, cut at the packet end E: dword j (window
@@ -450,7 +457,7 @@ struct SmallItem {
 
 // Fetch the windows of packets pb+gw (pb = the wave's first packet of the
 // step; pb >= n fetches nothing).
-template <int G, int U, int NT>
+template <int G, int U, int NT, bool SIDE = true>
 __device__ __forceinline__ void small_fetch(const BatchArgs &A,
                                             const SidePtrs &sp, uint64_t pb,
                                             uint32_t gw, uint32_t gl, bool ipv4,
@@ -471,31 +478,58 @@ __device__ __forceinline__ void small_fetch(const BatchArgs &A,
     const uint32_t cr = 16u * (gl + (uint32_t)u * G);
     it.c[u] = bld16(r, cr < eload ? lw + cr : kOOB, nt_step<NT>(u, U));
   }
-  it.sd = load_side(sp, active ? p : A.n - 1);
+  if (SIDE) it.sd = load_side(sp, active ? p : A.n - 1);
 }
 
-template <int G, int U, int NT>
+// PR (packets per run): 0 = wave w's step t takes packets (w + t*waves)*GPW on
+// (the grid's waves interleave over the batch); PR > 0 = wave w takes PR
+// consecutive packets in PR/GPW steps, then the run w + waves and so on. A
+// run's side records (PR * 8 or 2 bytes) come in with one load by lanes
+// 0..PR-1 when its first step is fetched, and its results leave in one store
+// (PR * 2 bytes) after its last step: per-step side loads and result stores
+// are small scattered requests, and a wave's loads return in order, so one
+// slow side load holds up the packet bytes behind it.
+template <int G, int U, int NT, int PR = 0>
 __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
   constexpr int GPW = 64 / G;
+  constexpr int SPR = PR ? PR / GPW : 1;  // steps per run
+  static_assert(PR == 0 || (PR % GPW == 0 && PR <= 64 && (SPR & (SPR - 1)) == 0),
+                "a run is whole wave steps and fits the wave's lanes");
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t gl = lane & (G - 1);
   const uint32_t gw = lane / G;
   const uint64_t wave = grid_wave(A.xcd);
-  const uint64_t step = (uint64_t)gridDim.x * (blockDim.x >> 6) * GPW;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const int mode = A.mode;
   const bool ipv4 = mode_is_ipv4(mode);
   const SidePtrs sp = side_ptrs(A);
   const uint32_t uf = A.uf;
+  // first packet of the wave's step t
+  auto first = [&](uint64_t t) -> uint64_t {
+    if (PR == 0) return (wave + t * nwaves) * GPW;
+    return (wave + t / SPR * nwaves) * PR + (t % SPR) * GPW;
+  };
 
-  uint64_t pb = wave * GPW;
+  uint64_t t = 0;
+  uint64_t pb = first(0);
   if (pb >= A.n) return;
-  SmallItem<G, U> it;
-  small_fetch<G, U, NT>(A, sp, pb, gw, gl, ipv4, it);
-  for (;;) {
-    const uint64_t pn = pb + step;
+  uint32_t res = 0;  // PR: lane s < PR collects the run's result s
+  Side rs, nrs;      // PR: the current / next run's side record of packet `lane`
+  auto run_side = [&](uint64_t q, Side &d) __attribute__((always_inline)) {
+    const uint64_t x = q + lane;  // lanes >= PR read the run's first record again
+    d = load_side(sp, lane < (uint32_t)PR && x < A.n ? x : (q < A.n ? q : A.n - 1));
+  };
+  // One step: issue the loads of the next step into `nx`, then sum `it` and
+  // finish its packets. Returns false when the wave has no next step. The
+  // loop below alternates two items instead of copying nx into it: a copy
+  // would wait for the prefetch to land before the back-edge.
+  auto step = [&](const SmallItem<G, U> &it, SmallItem<G, U> &nx) __attribute__((always_inline)) -> bool {
+    const uint64_t pn = first(t + 1);
     const bool more = pn < A.n;  // wave-uniform
-    SmallItem<G, U> nx;
-    small_fetch<G, U, NT>(A, sp, more ? pn : A.n, gw, gl, ipv4, nx);
+    const uint32_t k = (uint32_t)(t % SPR);
+    small_fetch<G, U, NT, PR == 0>(A, sp, more ? pn : A.n, gw, gl, ipv4, nx);
+    if (PR && k == 0 && t) rs = nrs;  // after the prefetch: the copy waits for nrs only
+    if (PR && k == SPR - 1 && more) run_side(pn, nrs);
 
     uint32_t E = it.sh + it.len;
     if (ipv4) {
@@ -519,14 +553,40 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
     const Junk j = make_junk(it.sh, E, mode);
     uint32_t jx[3];
     junk_take<__builtin_ctz(G)>(it.c[0], lane & ~(uint32_t)(G - 1), j, jx);
-    if (gl == G - 1 && p < A.n) {
+    if (PR == 0) {
+      if (gl == G - 1 && p < A.n) {
+        const uint32_t v = le_to_be(acc - junk_sum<false>(jx, j, 0u), it.sh & 1u);
+        finish_packet(A, p, v, it.len, it.sd,
+                      A.fill ? A.fill + p * A.stride : nullptr, E - it.sh);
+      }
+    } else {
+      // the group's side record, from the lane that loaded it for the run
+      const int src = (int)(k * GPW + gw);
+      Side sd;
+      sd.a = (uint32_t)__shfl((int)rs.a, src, 64);
+      sd.b = (uint32_t)__shfl((int)rs.b, src, 64);
+      sd.i = (uint16_t)__shfl((int)rs.i, src, 64);
+      // every lane computes; the group's last lane holds the true value
       const uint32_t v = le_to_be(acc - junk_sum<false>(jx, j, 0u), it.sh & 1u);
-      finish_packet(A, p, v, it.len, it.sd,
-                    A.fill ? A.fill + p * A.stride : nullptr, E - it.sh);
+      const uint32_t r = packet_value(A, v, it.len, sd);
+      if (gl == G - 1 && p < A.n && A.fill) store_field(A, r, A.fill + p * A.stride, E - it.sh);
+      const uint32_t got = (uint32_t)__shfl((int)r, (int)((lane % GPW) * G + G - 1), 64);
+      res = lane / GPW == k ? got : res;
+      if (k == SPR - 1 || !more) {
+        const uint64_t q = pb - (uint64_t)k * GPW + lane;  // the run's packet `lane`
+        if (lane < (uint32_t)PR && q < A.n && A.out) A.out[q] = (uint16_t)res;
+      }
     }
-    if (!more) break;
-    it = nx;
     pb = pn;
+    ++t;
+    return more;
+  };
+  SmallItem<G, U> a, b;
+  small_fetch<G, U, NT, PR == 0>(A, sp, pb, gw, gl, ipv4, a);
+  if (PR) run_side(pb, rs);
+  for (;;) {
+    if (!step(a, b)) break;
+    if (!step(b, a)) break;
   }
 }
 
@@ -1782,10 +1842,24 @@ struct Variant {
   uint32_t G;       // lanes per packet
   uint32_t ppw;     // packets per wave step
   KernelFn fill = nullptr;  // in-place fill instantiation, if it has its own
+  uint32_t run = 0;  // packets per wave run (k_small), 0 = ppw
+  // k_small without runs (PR = 0): the in-place fill, and batches too small to
+  // give every wave of the grid a whole run
+  KernelFn inter = nullptr;
 };
 
-#define YU_SMALL(G, U) \
-  {"k_small<" #G "," #U ">", 16u * G * U, {k_small<G, U, 0>, k_small<G, U, 1>, k_small<G, U, 2>}, G, 64u / G}
+// k_small runs of 16 packets per wave (one side-record load and one result
+// store per run): config 3 235-246 -> 235-240 us against the interleaved
+// mapping (PR = 0; equal on some boxes), 64-packet runs 248; 1M x 768 B 131.5
+// -> 122.6, x 3000 B 467.8 -> 450.7; 256K x 768 B 43.8 -> 35.0. The in-place
+// fill keeps the interleaved mapping (config 9: 313 vs 328 us with runs), and
+// so do batches of fewer than 8 runs per CU (see launch).
+// profiles/r02/kbench_ab_k_small_runs.log
+constexpr int kSmallRun = 16;
+#define YU_SMALL(G, U)                                                                     \
+  {"k_small<" #G "," #U ">", 16u * G * U,                                                  \
+   {k_small<G, U, 0, kSmallRun>, k_small<G, U, 1, kSmallRun>, k_small<G, U, 2, kSmallRun>}, \
+   G, 64u / G, nullptr, kSmallRun, k_small<G, U, 2, 0>}
 #define YU_TINY(G, FILL) \
   {"k_tiny<" #G ">", 16u * G, {k_tiny<G, 0>, k_tiny<G, 1>, k_tiny<G, 1>}, G, 64u, FILL}
 
@@ -2008,16 +2082,24 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_status(e);
   const uint64_t waves_per_block = 4;
-  const uint64_t ppw = v.ppw;
+  const uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu(v.G);
+  // k_small: runs from 8 runs per CU up (1500-B packets, runs vs interleaved:
+  // 16384 packets 8.0 vs 7.2 us, 32768 11.3 vs 12.5, 131072 35.3 vs 38.8; 768-B
+  // packets 6.6 vs 5.0, 7.5 vs 8.2, 19.7 vs 22.0; kbench_ab_k_small_runs.log)
+  // (YU_RUNS: 0 never, 2 whenever not filling — measurement only)
+  static const int runs_knob = env_int("YU_RUNS", 0, 2, 1);
+  const bool runs = v.run && !A.fill &&
+                    (runs_knob == 2 || (runs_knob == 1 && A.n / v.run >= 8u * (uint64_t)cu_count(dev)));
+  const uint64_t ppw = runs ? v.run : v.ppw;
   uint64_t waves = (A.n + ppw - 1) / ppw;
   uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
-  uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu(v.G);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   BatchArgs a = A;
   a.xcd = (uint32_t)use_xcd();
   a.small_waves = (uint32_t)cu_count(dev) * 4u * (uint32_t)seg_small_blocks();
-  const KernelFn k = A.fill && v.fill ? v.fill : v.fn[use_nt()];
+  KernelFn k = A.fill && v.fill ? v.fill : v.fn[use_nt()];
+  if (v.run && !runs) k = v.inter;
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
