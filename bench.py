@@ -77,13 +77,15 @@ class Workload:
             nbytes = n * self.L
             self.side = 8 * n  # addrs
             self.name = "config3: 1M x 1500-B TCP segments incl. pseudo-header (sendTCP field value)"
-        elif cfg in (4, 6, 7):
+        elif cfg in (4, 6, 7, 11):
             # 4: ragged 64..9000 B back-to-back, RAW with initial (BASELINE config 4)
             # 6: tun RX burst, 1M whole IPv4 datagrams U{40..1500} B, VERIFY_RX (§8f row 1)
             # 7: the same with small datagrams U{40..200} B (ACKs, DNS, VoIP)
-            self.mode = batch.RAW if cfg == 4 else batch.VERIFY_RX
+            # 11: tun TX burst, 1M outgoing TCP/IPv4 datagrams U{40..1500} B, both
+            #     checksum fields (TX_DATAGRAM, two results per datagram)
+            self.mode = {4: batch.RAW, 11: batch.TX_DATAGRAM}.get(cfg, batch.VERIFY_RX)
             rng = np.random.default_rng(cfg)
-            hi = {4: 9001, 6: 1501, 7: 201}[cfg]
+            hi = {4: 9001, 6: 1501, 7: 201, 11: 1501}[cfg]
             lens = rng.integers(64 if cfg == 4 else 40, hi, size=n)
             offs = np.zeros(n + 1, dtype=np.int64)
             offs[1:] = np.cumsum(lens)
@@ -94,7 +96,9 @@ class Workload:
             self.side = 8 * (n + 1) + (2 * n if cfg == 4 else 0)
             self.name = ("config4: ragged 1M packets U{64..9000} B back-to-back (odd offsets)" if cfg == 4 else
                          f"tun RX: 1M received IPv4 datagrams U{{40..{hi - 1}}} B back-to-back, header + TCP "
-                         "checksum verification (VERIFY_RX)")
+                         "checksum verification (VERIFY_RX)" if cfg != 11 else
+                         "tun TX: 1M outgoing TCP/IPv4 datagrams U{40..1500} B back-to-back, IPv4 header and "
+                         "TCP checksum fields (TX_DATAGRAM, 2 results per datagram)")
         else:
             raise SystemExit(f"unknown config {cfg}")
         self.payload = nbytes
@@ -106,12 +110,14 @@ class Workload:
                 v = d.view(n, self.L)
                 v[:, 12] = 0x50
                 v[:, 16:18] = 0
-            if cfg in (6, 7):  # IPv4 header: IHL 5, TotalLength = packet length, protocol TCP
+            if cfg in (6, 7, 11):  # IPv4 header: IHL 5, TotalLength = packet length, protocol TCP
                 s0 = self.offsets[:-1]
                 d[s0] = 0x45
                 d[s0 + 2] = (self.lens >> 8).to(torch.uint8)
                 d[s0 + 3] = (self.lens & 0xFF).to(torch.uint8)
                 d[s0 + 9] = 6
+                if cfg == 11:  # the TCP segment as sendTCP encodes it: DataOffset 5
+                    d[s0 + 32] = 0x50
             self.data.append(d)
         if cfg == 2 or cfg == 4:
             self.initial_arr = torch.randint(0, 65536, (n,), dtype=torch.int32, device=dev,
@@ -120,12 +126,12 @@ class Workload:
             self.name += "; fused in-place field writer (yu_csum_fill_uniform, no uint16 array)"
         if base in (3, 8):
             self.addrs = torch.randint(0, 256, (8 * n,), dtype=torch.uint8, device=dev, generator=g)
-        self.out = torch.empty(n, dtype=torch.uint16, device=dev)
+        self.out = torch.empty(n * batch.outputs(self.mode), dtype=torch.uint16, device=dev)
         if self.offsets is not None:  # validate once; the timed launches skip the check
             batch.checksum_ragged(self.data[0], self.offsets, self.mode,
                                   initial_arr=self.initial_arr, out=self.out)
         # algorithmic bytes per launch: payload + side arrays + uint16 out
-        self.bytes = self.payload + self.side + 2 * n
+        self.bytes = self.payload + self.side + 2 * n * batch.outputs(self.mode)
 
     def step(self, k: int) -> None:
         d = self.data[k % self.R]
@@ -226,7 +232,7 @@ def cpu_baseline(w: Workload, threads: int, budget_s: float):
             o = offs[:sample_pk + 1]
             run = lambda: C.batch(host, w.mode, offsets=o, initial_arr=ia, threads=nthreads)  # noqa: E731
             b = int(o[-1] - o[0])
-        b_alg = b + (w.side + 2 * w.n) * sample_pk / w.n
+        b_alg = b + (w.side + 2 * w.n * batch.outputs(w.mode)) * sample_pk / w.n
         reps, t = 0, 0.0
         t0 = time.perf_counter()
         while t < budget_s / 2 or reps < 2:
@@ -359,7 +365,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 6, 7, 8, 9, 10])
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 6, 7, 8, 9, 10, 11])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip configs 2/4 side measurements")
     ap.add_argument("--cpu-budget", type=float, default=6.0, help="wall seconds for the CPU baseline")
@@ -418,7 +424,7 @@ def main():
             "workload": w.name,
             "packets_per_gpu": w.n,
             "packet_bytes": w.L if w.L else "U{64..9000}",
-            "mode": {0: "raw", 1: "udp", 2: "tcp", 8: "verify_rx"}.get(w.mode, str(w.mode)),
+            "mode": {0: "raw", 1: "udp", 2: "tcp", 8: "verify_rx", 9: "tx_datagram"}.get(w.mode, str(w.mode)),
             "algorithmic_bytes_per_step_per_gpu": w.bytes,
             "rotating_batches": w.R,
             "kernel": w.kernel_name(),
@@ -439,7 +445,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_extra:
         extra = {}
-        for c in (2, 8, 3, 4, 6, 7, 9, 10):
+        for c in (2, 8, 3, 4, 6, 7, 9, 10, 11):
             if c == args.config:
                 continue
             wc = Workload(c, dev, seed=77 + c)

@@ -84,7 +84,19 @@ const (
 	ModeVerifyTCP  Mode = C.YU_MODE_VERIFY_TCP
 	ModeVerifyUDP  Mode = C.YU_MODE_VERIFY_UDP
 	ModeVerifyRX   Mode = C.YU_MODE_VERIFY_RX // out[i] = RX* bits
+	// whole outgoing IPv4 datagrams: out[2i] = IPv4 header field, out[2i+1] =
+	// transport field (two results per packet, see Outputs)
+	ModeTxDatagram Mode = C.YU_MODE_TX_DATAGRAM
 )
+
+// Outputs is the number of results per packet a mode writes to out
+// (include/yucsum.h YU_MODE_OUTPUTS): 2 for ModeTxDatagram, else 1.
+func (m Mode) Outputs() uint64 {
+	if m == ModeTxDatagram {
+		return 2
+	}
+	return 1
+}
 
 // VERIFY_RX result bits (include/yucsum.h YU_RX_*).
 const (
@@ -107,7 +119,7 @@ func BatchHostUniform(data []byte, stride uint64, length uint32, n uint64, mode 
 		return nil
 	}
 	// overflow-safe form of (n-1)*stride+length <= len(data)
-	if uint64(len(out)) < n || uint64(length) > uint64(len(data)) ||
+	if uint64(len(out))/mode.Outputs() < n || uint64(length) > uint64(len(data)) ||
 		(n > 1 && stride > (uint64(len(data))-uint64(length))/(n-1)) {
 		return errTooSmall
 	}
@@ -185,7 +197,7 @@ func BatchHostRagged(data []byte, offsets []uint64, mode Mode, initial []uint16,
 		return nil
 	}
 	n := uint64(len(offsets) - 1)
-	if uint64(len(out)) < n || offsets[n] > uint64(len(data)) {
+	if uint64(len(out))/mode.Outputs() < n || offsets[n] > uint64(len(data)) {
 		return errTooSmall
 	}
 	if err := checkSide(n, initial, addrs); err != nil {
@@ -209,7 +221,7 @@ func BatchHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, 
 	if len(pkts) == 0 {
 		return nil
 	}
-	if len(out) < len(pkts) {
+	if uint64(len(out))/mode.Outputs() < uint64(len(pkts)) {
 		return errTooSmall
 	}
 	if err := checkSide(uint64(len(pkts)), initial, addrs); err != nil {
@@ -228,7 +240,8 @@ func BatchHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, 
 // it computes the checksum and stores it big-endian into the packet's field
 // in place, like SetChecksum (header/udp.go:60-62, header/tcp.go:156-158,
 // header/ipv4.go:165-167, header/icmpv4.go:46-48). mode is ModeUDP, ModeTCP,
-// ModeIPv4 or ModeICMP; out (len n) may be nil.
+// ModeIPv4, ModeICMP or ModeTxDatagram (both fields of whole datagrams); out
+// (n results, 2n for ModeTxDatagram) may be nil.
 func FillHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, out []uint16,
 	device int) error {
 	if len(pkts) == 0 {
@@ -236,7 +249,7 @@ func FillHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, o
 	}
 	var po *C.uint16_t
 	if out != nil {
-		if len(out) < len(pkts) {
+		if uint64(len(out))/mode.Outputs() < uint64(len(pkts)) {
 			return errTooSmall
 		}
 		po = (*C.uint16_t)(unsafe.Pointer(&out[0]))

@@ -143,7 +143,32 @@ uint16_t yu_pseudo_header_checksum(uint32_t protocol,
  *            pseudo-header and length (network/ipv4/icmp.go:36-45).
  * out[i] is a bit set of YU_RX_*. No side arrays; not a fill mode. */
 #define YU_MODE_VERIFY_RX 8
-#define YU_MODE_COUNT 9
+/* Transmit side of whole IPv4 datagrams as the link endpoint writes them
+ * (network/ipv4/ipv4.go:80-97 WritePacket after sendUDP
+ * transport/udp/endpoint.go:164-187, sendTCP transport/tcp/connect.go:556-586
+ * or sendICMPv4 network/ipv4/icmp.go:36-45; written out by
+ * link/tundev/tundev.go:171-196): both checksum fields of a datagram in one
+ * pass, all inputs taken from the datagram itself. TWO results per packet:
+ *   out[2i]   = the IPv4 header checksum WritePacket stores: YU_MODE_IPV4's
+ *               value, ^Checksum(b[:HeaderLength()]) with the field as 0;
+ *   out[2i+1] = the transport checksum its sender stores, over the segment
+ *               b[HeaderLength():TotalLength()] with the pseudo-header from
+ *               the datagram's source, destination and protocol and the
+ *               length TotalLength() - HeaderLength(): YU_MODE_UDP (17),
+ *               YU_MODE_TCP (6) or YU_MODE_ICMP (1) on that segment, field as
+ *               0; 0 when the protocol is another one or the segment is
+ *               shorter than its header (8 / 20 / 4 bytes).
+ * Datagrams must satisfy 20 <= HeaderLength() <= TotalLength() <= len (every
+ * datagram WritePacket encodes: IHL 5); others get {0, 0} and, in place,
+ * no write. TCP segments need 20 <= DataOffset() <= their length (as
+ * YU_MODE_TCP). With fill, each field whose value is defined is stored
+ * big-endian in place. No side arrays (initial / addrs are ignored). */
+#define YU_MODE_TX_DATAGRAM 9
+#define YU_MODE_COUNT 10
+
+/* Results per packet in `out`: 2 for YU_MODE_TX_DATAGRAM, 1 otherwise. Every
+ * out / h_out array below holds n * YU_MODE_OUTPUTS(mode) uint16 values. */
+#define YU_MODE_OUTPUTS(mode) ((mode) == YU_MODE_TX_DATAGRAM ? 2 : 1)
 
 #define YU_RX_IP_OK 1u   /* header checksum verifies */
 #define YU_RX_L4 2u      /* transport (TCP/UDP/ICMP) present and checked */
@@ -172,8 +197,9 @@ uint16_t yu_pseudo_header_checksum(uint32_t protocol,
  *  initial_arr: NULL or n uint16 (per-packet initial / pseudo partial)
  *  initial:     used when initial_arr == NULL
  *  addrs:       NULL or n*8 bytes {src[4], dst[4]} (UDP/TCP/VERIFY_TCP/UDP)
- *  out:         n uint16 results, written in host byte order as a number
- *               (store it big-endian into the packet to set the field). */
+ *  out:         n * YU_MODE_OUTPUTS(mode) uint16 results, written in host
+ *               byte order as numbers (store one big-endian into the packet
+ *               to set its field). */
 int yu_csum_batch_uniform(const uint8_t *data, uint64_t stride, uint32_t len,
                           uint64_t n, int mode,
                           const uint16_t *initial_arr, uint16_t initial,
@@ -188,11 +214,12 @@ int yu_csum_batch_ragged(const uint8_t *data, const uint64_t *offsets,
                          const uint16_t *initial_arr, uint16_t initial,
                          const uint8_t *addrs, uint16_t *out, void *stream);
 
-/* In-place field writer (TX modes UDP/TCP/IPV4/ICMP only): computes the
- * same value as the matching batch call and stores it big-endian into the
- * packet's checksum field (UDP.SetChecksum header/udp.go:60-62,
- * TCP.SetChecksum header/tcp.go:156-158, IPv4.SetChecksum
- * header/ipv4.go:165-167, ICMPv4.SetChecksum header/icmpv4.go:46-48).
+/* In-place field writer (TX modes UDP/TCP/IPV4/ICMP/TX_DATAGRAM only):
+ * computes the same value as the matching batch call and stores it
+ * big-endian into the packet's checksum field (UDP.SetChecksum
+ * header/udp.go:60-62, TCP.SetChecksum header/tcp.go:156-158,
+ * IPv4.SetChecksum header/ipv4.go:165-167, ICMPv4.SetChecksum
+ * header/icmpv4.go:46-48; both fields of a datagram in TX_DATAGRAM).
  * `out` may be NULL. `data` is written. */
 int yu_csum_fill_uniform(uint8_t *data, uint64_t stride, uint32_t len,
                          uint64_t n, int mode,
@@ -246,7 +273,7 @@ int yu_csum_batch_host_iov(const yu_iovec *iov, const uint64_t *first_iov,
                            uint16_t *h_out, int device);
 
 /* Host-memory field writer: the matching yu_csum_batch_host_* call (TX modes
- * UDP/TCP/IPV4/ICMP only), then each result stored big-endian into the
+ * UDP/TCP/IPV4/ICMP/TX_DATAGRAM only), then each result stored big-endian into the
  * packet's checksum field in host memory, as the device writer does
  * (yu_csum_fill_uniform). `h_out` may be NULL. The iov form writes through
  * the views (their `base` must be writable memory). Synchronous. */

@@ -38,6 +38,7 @@
 #define OR_MODE_VERIFY_TCP 6
 #define OR_MODE_VERIFY_UDP 7
 #define OR_MODE_VERIFY_RX 8
+#define OR_MODE_TX_DATAGRAM 9
 #define OR_RX_IP_OK 1
 #define OR_RX_L4 2
 #define OR_RX_L4_OK 4
@@ -220,14 +221,56 @@ uint16_t or_packet(int mode, const uint8_t *pkt, uint64_t len,
   }
 }
 
+/* A whole outgoing IPv4 datagram (YU_MODE_TX_DATAGRAM, include/yucsum.h):
+ * the two fields the reference's senders store before the link endpoint
+ * writes it (network/ipv4/ipv4.go:80-97 after transport/udp/endpoint.go:
+ * 164-187, transport/tcp/connect.go:556-586 or network/ipv4/icmp.go:36-45),
+ * each composed exactly as the single-field modes above, with the pseudo
+ * header taken from the datagram's own addresses and protocol. res[0] = IPv4
+ * header field, res[1] = transport field; {0, 0} outside the contract
+ * 20 <= HeaderLength() <= TotalLength() <= len. */
+void or_tx_datagram(const uint8_t *pkt, uint64_t len, uint16_t res[2]) {
+  res[0] = res[1] = 0;
+  if (len < 20) return;
+  size_t hl = (size_t)(pkt[0] & 0xf) * 4;     /* HeaderLength() */
+  size_t tl = ((size_t)pkt[2] << 8) | pkt[3]; /* TotalLength() */
+  if (hl < 20 || hl > tl || tl > len) return;
+  res[0] = or_packet(OR_MODE_IPV4, pkt, len, NULL, 0, NULL, 0);
+  const uint8_t *seg = pkt + hl;                /* Payload() */
+  uint64_t slen = tl - hl;
+  const uint8_t *rec = pkt + 12;                /* {src[4], dst[4]}: types/route.go:90-92 */
+  switch (pkt[9]) {                             /* Protocol() */
+    case 17:
+      if (slen >= 8) res[1] = or_packet(OR_MODE_UDP, seg, slen, NULL, 0, rec, 0);
+      break;
+    case 6:
+      if (slen >= 20) res[1] = or_packet(OR_MODE_TCP, seg, slen, NULL, 0, rec, 0);
+      break;
+    case 1:
+      if (slen >= 4) res[1] = or_packet(OR_MODE_ICMP, seg, slen, NULL, 0, NULL, 0);
+      break;
+    default:
+      break;
+  }
+}
+
+/* Results per packet: 2 for TX_DATAGRAM (out[2p], out[2p+1]), else 1. */
+static void or_one(int mode, const uint8_t *pkt, uint64_t len,
+                   const uint16_t *initial_arr, uint16_t initial,
+                   const uint8_t *addrs, uint16_t *out, uint64_t p) {
+  if (mode == OR_MODE_TX_DATAGRAM)
+    or_tx_datagram(pkt, len, out + 2 * p);
+  else
+    out[p] = or_packet(mode, pkt, len, initial_arr, initial, addrs, p);
+}
+
 void or_batch_uniform(const uint8_t *data, uint64_t stride, uint32_t len,
                       uint64_t n, int mode, const uint16_t *initial_arr,
                       uint16_t initial, const uint8_t *addrs, uint16_t *out,
                       uint64_t first, uint64_t count) {
   (void)n;
   for (uint64_t p = first; p < first + count; ++p)
-    out[p] = or_packet(mode, data + p * stride, len, initial_arr, initial,
-                       addrs, p);
+    or_one(mode, data + p * stride, len, initial_arr, initial, addrs, out, p);
 }
 
 void or_batch_ragged(const uint8_t *data, const uint64_t *offsets, uint64_t n,
@@ -236,8 +279,8 @@ void or_batch_ragged(const uint8_t *data, const uint64_t *offsets, uint64_t n,
                      uint64_t count) {
   (void)n;
   for (uint64_t p = first; p < first + count; ++p)
-    out[p] = or_packet(mode, data + offsets[p], offsets[p + 1] - offsets[p],
-                       initial_arr, initial, addrs, p);
+    or_one(mode, data + offsets[p], offsets[p + 1] - offsets[p], initial_arr,
+           initial, addrs, out, p);
 }
 
 /* ---- static even split over host threads (cpu_baseline leg) ---- */

@@ -32,12 +32,18 @@ LIB_PATH = os.path.join(HERE, "build", "libcsum_oracle.so")
 
 MODE_RAW, MODE_UDP, MODE_TCP, MODE_IPV4, MODE_ICMP = 0, 1, 2, 3, 4
 MODE_VERIFY_IPV4, MODE_VERIFY_TCP, MODE_VERIFY_UDP, MODE_VERIFY_RX = 5, 6, 7, 8
+MODE_TX_DATAGRAM = 9
 MODE_NAMES = {
     MODE_RAW: "raw", MODE_UDP: "udp", MODE_TCP: "tcp", MODE_IPV4: "ipv4",
     MODE_ICMP: "icmp", MODE_VERIFY_IPV4: "verify_ipv4",
     MODE_VERIFY_TCP: "verify_tcp", MODE_VERIFY_UDP: "verify_udp",
-    MODE_VERIFY_RX: "verify_rx",
+    MODE_VERIFY_RX: "verify_rx", MODE_TX_DATAGRAM: "tx_datagram",
 }
+
+
+def outputs(mode: int) -> int:
+    """Results per packet (include/yucsum.h YU_MODE_OUTPUTS)."""
+    return 2 if mode == MODE_TX_DATAGRAM else 1
 RX_IP_OK, RX_L4, RX_L4_OK, RX_INVALID = 1, 2, 4, 8  # include/yucsum.h YU_RX_*
 
 
@@ -184,22 +190,55 @@ def packet(mode: int, pkt: bytes, initial_arr=None, initial: int = 0, addrs=None
     raise ValueError(f"bad mode {mode}")
 
 
+def _one(mode, pkt, initial_arr, initial, addrs, p):
+    if mode == MODE_TX_DATAGRAM:
+        return list(tx_datagram(pkt))
+    return [packet(mode, pkt, initial_arr, initial, addrs, p)]
+
+
 def batch_uniform_py(data, stride, length, n, mode, initial_arr=None, initial=0, addrs=None):
     data = bytes(data)
-    return np.array([packet(mode, data[p * stride: p * stride + length], initial_arr, initial, addrs, p)
-                     for p in range(n)], dtype=np.uint16)
+    return np.array([v for p in range(n)
+                     for v in _one(mode, data[p * stride: p * stride + length], initial_arr, initial, addrs, p)],
+                    dtype=np.uint16)
 
 
 def batch_ragged_py(data, offsets, mode, initial_arr=None, initial=0, addrs=None):
     data = bytes(data)
     n = len(offsets) - 1
-    return np.array([packet(mode, data[int(offsets[p]): int(offsets[p + 1])], initial_arr, initial, addrs, p)
-                     for p in range(n)], dtype=np.uint16)
+    return np.array([v for p in range(n)
+                     for v in _one(mode, data[int(offsets[p]): int(offsets[p + 1])], initial_arr, initial,
+                                   addrs, p)], dtype=np.uint16)
 
 
 # --------------------------------------------------------------------------
 # C restatement (ctypes)
 # --------------------------------------------------------------------------
+def tx_datagram(pkt: bytes) -> tuple[int, int]:
+    """YU_MODE_TX_DATAGRAM (include/yucsum.h): the IPv4 header field WritePacket
+    stores (network/ipv4/ipv4.go:80-97) and the transport field its sender stores
+    (transport/udp/endpoint.go:164-187, transport/tcp/connect.go:556-586,
+    network/ipv4/icmp.go:36-45) for a whole outgoing datagram, the pseudo header
+    from its own addresses; (0, 0) outside 20 <= HeaderLength <= TotalLength <= len."""
+    pkt = bytes(pkt)
+    if len(pkt) < 20:
+        return 0, 0
+    hl = (pkt[0] & 0xF) * 4
+    tl = (pkt[2] << 8) | pkt[3]
+    if hl < 20 or hl > tl or tl > len(pkt):
+        return 0, 0
+    ip = packet(MODE_IPV4, pkt)
+    seg, rec, proto = pkt[hl:tl], np.frombuffer(pkt[12:20], np.uint8), pkt[9]
+    l4 = 0
+    if proto == 17 and len(seg) >= 8:
+        l4 = packet(MODE_UDP, seg, addrs=rec)
+    elif proto == 6 and len(seg) >= 20:
+        l4 = packet(MODE_TCP, seg, addrs=rec)
+    elif proto == 1 and len(seg) >= 4:
+        l4 = packet(MODE_ICMP, seg)
+    return ip, l4
+
+
 class _C:
     def __init__(self, path: str = LIB_PATH):
         if not os.path.exists(path):
@@ -239,7 +278,8 @@ class _C:
             offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
             n = len(offsets) - 1
         assert n is not None
-        out = np.zeros(max(n, 1), dtype=np.uint16)
+        k = outputs(mode)
+        out = np.zeros(max(n * k, 1), dtype=np.uint16)
         ia = None if initial_arr is None else np.ascontiguousarray(initial_arr, dtype=np.uint16)
         ad = None if addrs is None else np.ascontiguousarray(addrs, dtype=np.uint8)
         rc = self.lib.or_batch_mt(data.ctypes.data, None if offsets is None else offsets.ctypes.data,
@@ -248,7 +288,7 @@ class _C:
                                   out.ctypes.data, threads)
         if rc != 0:
             raise RuntimeError("oracle batch failed")
-        return out[:n]
+        return out[:n * k]
 
 
 _c_singleton = None

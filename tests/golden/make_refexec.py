@@ -100,6 +100,34 @@ class Ref:
         hdr[2:4] = b"\x00\x00"
         return ~self.checksum(bytes(hdr), self.checksum(bytes(msg[4:]), 0)) & 0xFFFF
 
+    def tx_datagram(self, pkt: bytes) -> list:
+        """YU_MODE_TX_DATAGRAM (include/yucsum.h): a whole outgoing datagram's two
+        fields — ipv4.WritePacket's header field (network/ipv4/ipv4.go:85-94) and the
+        transport field its sender stored before (sendUDP / sendTCP / sendICMPv4),
+        with the route addresses = the header's SourceAddress / DestinationAddress
+        (ipv4.go:84-92 encodes them from the same route) over Payload()."""
+        if len(pkt) < 20:
+            return [0, 0]
+        hl = self.m("IPv4", pkt, "HeaderLength").v
+        tl = self.m("IPv4", pkt, "TotalLength").v
+        if hl < 20 or not self.m("IPv4", pkt, "IsValid", G.Int(len(pkt), "int")):
+            return [0, 0]
+        ip = self.ipv4_field(pkt)
+        proto = self.m("IPv4", pkt, "Protocol").v
+        seg = self.m("IPv4", pkt, "Payload").bytes()
+        assert len(seg) == tl - hl
+        # SourceAddress() / DestinationAddress() are b[12:16] / b[16:20]
+        # (header/ipv4.go:111-118; their types.Address is outside goexec's packages)
+        src, dst = pkt[12:16], pkt[16:20]
+        l4 = 0
+        if proto == 17 and len(seg) >= 8:
+            l4 = self.udp_field(seg, src, dst)
+        elif proto == 6 and len(seg) >= 20:
+            l4 = self.tcp_field(seg, src, dst)
+        elif proto == 1 and len(seg) >= 4:
+            l4 = self.icmp_field(seg)
+        return [ip, l4]
+
     # --- receive-side verification (checker semantics) ------------------------------
     def verify_ipv4(self, pkt: bytes) -> int:
         """checker/checker.go:32-35: the sum over b[:HeaderLength()] incl. the field."""
@@ -245,6 +273,24 @@ def main() -> None:
     for i in range(len(offs) - 1):
         pk = bytes(blob[int(offs[i]):int(offs[i + 1])])
         add(O.MODE_VERIFY_RX, pk, bytes(8), ref.rx_flags(pk))
+    # whole outgoing datagrams (TX_DATAGRAM): built like the reference senders, their
+    # checksum fields then overwritten with garbage (the mode takes them as 0), plus
+    # out-of-contract ones (IHL < 5, lengths that do not fit, other protocols)
+    for i in range(120):
+        pk = bytearray(rxgen.make_packet(nrng, int(nrng.integers(0, 1480)),
+                                         ihl=5 if i % 3 else None))
+        hl = (pk[0] & 0xF) * 4
+        pk[10:12] = rnd(rng, 2)
+        f = {17: 6, 6: 16, 1: 2}.get(pk[9])
+        if f is not None:
+            pk[hl + f: hl + f + 2] = rnd(rng, 2)
+        if i % 10 == 9:
+            pk = rxgen.tcp_contract(rxgen.damage(nrng, pk))
+        add(O.MODE_TX_DATAGRAM, bytes(pk), bytes(8), ref.tx_datagram(bytes(pk)))
+    for ihl in (0, 1, 4):  # HeaderLength() under 20: outside the contract
+        pk = bytearray(rxgen.make_packet(nrng, 40, proto=17, ihl=5))
+        pk[0] = 0x40 | ihl
+        add(O.MODE_TX_DATAGRAM, bytes(pk), bytes(8), ref.tx_datagram(bytes(pk)))
     out["modes"] = modes
 
     # oracle agreement on every mode vector (ragged batch through the C oracle)
@@ -258,7 +304,7 @@ def main() -> None:
         init = np.array([int.from_bytes(bytes.fromhex(v["addrs"])[:2], "little") for v in vecs], np.uint16)
         got = C.batch(data, m, offsets=offs, addrs=ad if m in (1, 2, 6, 7) else None,
                       initial_arr=init if m == O.MODE_RAW else None)
-        want = np.array([v["want"] for v in vecs], np.uint16)
+        want = np.array([v["want"] for v in vecs], np.uint16).reshape(-1)
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (mode, bad[:5], got[bad[:5]], want[bad[:5]])
 

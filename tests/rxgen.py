@@ -129,8 +129,56 @@ def filler_packet(rng, total):
     return pkt
 
 
-def tile_edge_batch(rng, n, chunk, base_off, tile=4096):
-    """Ragged RX batch whose short-header packets (short_header_packet) start so that
+def tx_packet(rng, plen, proto=None, ihl=None, pad4=False):
+    """An outgoing datagram for TX_DATAGRAM: built like the reference's senders
+    (make_packet), then both checksum fields overwritten with random bytes (the
+    mode takes them as 0). pad4: trailing bytes up to a multiple of 4 (past
+    TotalLength, which the contract allows), for the in-place writer's 4-aligned
+    offsets."""
+    pkt = make_packet(rng, plen, proto=proto, ihl=ihl)
+    hl = (pkt[0] & 0xF) * 4
+    pkt[10:12] = rng.integers(0, 256, size=2, dtype=np.uint8).tobytes()
+    f = {17: 6, 6: 16, 1: 2}.get(pkt[9])
+    if f is not None:
+        pkt[hl + f: hl + f + 2] = rng.integers(0, 256, size=2, dtype=np.uint8).tobytes()
+    if pad4 and len(pkt) % 4:
+        pkt += rng.integers(0, 256, size=4 - len(pkt) % 4, dtype=np.uint8).tobytes()
+    return pkt
+
+
+def tcp_contract(pkt):
+    """Keep a damaged outgoing datagram inside YU_MODE_TCP's contract (20 <=
+    DataOffset <= segment length, as every segment sendTCP encodes): a flipped
+    header byte can move the segment so that its DataOffset byte is payload. The
+    datagram may still leave the IPv4 contract (its fields are then not set)."""
+    if len(pkt) >= 20:
+        hl, tl = (pkt[0] & 0xF) * 4, (pkt[2] << 8) | pkt[3]
+        if 20 <= hl <= tl <= len(pkt) and pkt[9] == 6 and tl - hl >= 20:
+            doff = (pkt[hl + 12] >> 4) * 4
+            if doff < 20 or doff > tl - hl:
+                pkt[hl + 12] = 0x50 | (pkt[hl + 12] & 0x0F)
+    return pkt
+
+
+def tx_batch(rng, n, lo=0, hi=1480, bad=0.1, pad4=False):
+    """Ragged blob + offsets of n outgoing datagrams (tx_packet), a share of them
+    damaged or malformed (damage: some leave the TX contract, some do not)."""
+    pkts = []
+    for _ in range(n):
+        p = tx_packet(rng, int(rng.integers(lo, hi + 1)), pad4=pad4)
+        if rng.random() < bad:
+            p = tcp_contract(damage(rng, p))
+            if pad4 and len(p) % 4:
+                p += bytes(4 - len(p) % 4)
+        pkts.append(bytes(p))
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in pkts])
+    return np.frombuffer(b"".join(pkts), dtype=np.uint8).copy(), offs
+
+
+def tile_edge_batch(rng, n, chunk, base_off, tile=4096, special=None):
+    """Ragged RX batch whose short-header packets (short_header_packet, or
+    `special(rng, total)`) start so that
     floor4(start) lies 4..20 bytes before a tile boundary of k_seg's chunk-relative
     tiling (b0 = floor4 of the chunk's first start; boundaries every `tile` bytes,
     both the 4 KiB and the 8 KiB ones). Each is preceded by a filler sized to put
@@ -143,7 +191,7 @@ def tile_edge_batch(rng, n, chunk, base_off, tile=4096):
         if i % chunk == 0:
             b0 = pos & ~3
         if special_next:
-            p = short_header_packet(rng, int(rng.integers(20, 81)))
+            p = (special or short_header_packet)(rng, int(rng.integers(20, 81)))
             special_next = False
         else:
             d = 4 * int(rng.integers(1, 6))

@@ -125,7 +125,7 @@ def test_argument_validation_precedes_device():
     first = (ctypes.c_uint64 * 2)(0, 2)
     assert L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 1, 0, None, 0, None,
                                     o, 0) == _lib.YU_EINVAL
-    assert L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 1, 9, None, 0, None,
+    assert L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 1, 10, None, 0, None,
                                     o, 0) == _lib.YU_EINVAL  # mode
     # multi-GPU host calls: device list and batch checked before any device work
     devs = (ctypes.c_int * 2)(0, 0)

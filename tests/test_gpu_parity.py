@@ -273,6 +273,142 @@ def test_verify_rx_fuzz(dev, oracle_c):
         assert {"k_loop<4,rx>", "k_seg<8,rx,c16>", "k_seg<8,rx>"} <= seen, seen
 
 
+def _tx_expected(blob, offs, want, length=None):
+    """The bytes TX_DATAGRAM's in-place writer must leave: every byte as before,
+    except the two fields of each datagram where they are defined (the oracle's
+    values, include/yucsum.h YU_MODE_TX_DATAGRAM). Datagram i starts at offs[i]
+    and ends at offs[i+1], or after `length` bytes (uniform slots). Also returns
+    which datagrams got an IPv4 and which a transport field."""
+    exp = blob.copy()
+    n = len(offs) - 1
+    ip_def, l4_def = np.zeros(n, bool), np.zeros(n, bool)
+    for i in range(n):
+        a = int(offs[i])
+        e = int(offs[i + 1]) if length is None else a + length
+        pk = blob[a:e]
+        if e - a < 20:
+            continue
+        hl, tl = (int(pk[0]) & 15) * 4, (int(pk[2]) << 8) | int(pk[3])
+        if hl < 20 or hl > tl or tl > e - a:
+            continue
+        exp[a + 10], exp[a + 11] = want[2 * i] >> 8, want[2 * i] & 0xFF
+        ip_def[i] = True
+        fo, mn = {17: (6, 8), 6: (16, 20), 1: (2, 4)}.get(int(pk[9]), (0, 0))
+        if fo and tl - hl >= mn:
+            exp[a + hl + fo], exp[a + hl + fo + 1] = want[2 * i + 1] >> 8, want[2 * i + 1] & 0xFF
+            l4_def[i] = True
+    return exp, ip_def, l4_def
+
+
+@pytest.mark.parametrize("npk", [1, 64, 4096, 4097, 65535, 65536, 70000])
+def test_tx_datagram_ragged(dev, oracle_c, npk):
+    """TX_DATAGRAM over ragged batches of outgoing datagrams on both sides of every
+    kernel cut-over (a wave per datagram up to 4096, 16-datagram k_seg chunks up to
+    65535, 64-datagram chunks from 65536): both fields against the oracle at an odd
+    start, then in place at 4-aligned offsets, where afterwards only the defined
+    fields differ from the input and the filled datagrams pass VERIFY_RX."""
+    import rxgen
+    rng = np.random.default_rng(9500 + npk)
+    hi = 1480 if npk <= 4097 else 200
+    blob, offs = rxgen.tx_batch(rng, npk, lo=0, hi=hi, bad=0.15, pad4=True)
+    if npk > 1000:  # a few jumbo datagrams among the small ones (past a tile)
+        jb, jo = rxgen.tx_batch(rng, 8, lo=5000, hi=9000, bad=0.0, pad4=True)
+        blob = np.concatenate([jb, blob])
+        offs = np.concatenate([jo[:-1], offs + jo[-1]])
+        npk += 8
+    want = oracle_c.batch(blob, O.MODE_TX_DATAGRAM, offsets=offs)
+    assert want.size == 2 * npk
+    assert (want[0::2] != 0).mean() > 0.8 and (want[1::2] != 0).mean() > 0.5
+    for base_off in (1, 3):
+        b = np.concatenate([np.zeros(base_off, np.uint8), blob, np.zeros(32, np.uint8)])
+        got = batch.checksum_ragged(_to(dev, b), _to(dev, (offs + base_off).view(np.int64)),
+                                    "tx_datagram").cpu().numpy()
+        assert np.array_equal(got, want), (base_off, np.nonzero(got != want)[0][:10])
+    d = _to(dev, np.concatenate([blob, np.zeros(32, np.uint8)]))
+    o = _to(dev, offs.view(np.int64))
+    got = batch.checksum_ragged(d, o, "tx_datagram", fill=True).cpu().numpy()
+    assert np.array_equal(got, want)
+    filled = d.cpu().numpy()[:blob.size]
+    exp, ip_def, l4_def = _tx_expected(blob, offs, want)
+    bad = np.nonzero(filled != exp)[0]
+    assert bad.size == 0, bad[:10]
+    assert ip_def.mean() > 0.8 and l4_def.mean() > 0.5
+    # what was filled now verifies (checker.IPv4 / checker.TCP semantics)
+    rx = batch.checksum_ragged(d, o, "verify_rx").cpu().numpy()
+    assert (rx[ip_def] & O.RX_IP_OK).all()
+    assert (rx[l4_def] & (O.RX_L4 | O.RX_L4_OK) == (O.RX_L4 | O.RX_L4_OK)).all()
+
+
+@pytest.mark.parametrize("npk,kern", [(5000, "k_seg<8,dg,c16>"), (66000, "k_seg<8,dg>")])
+def test_tx_datagram_header_straddles_tile(dev, oracle_c, npk, kern):
+    """k_seg's DG kind gathers each datagram's first 20 header bytes across tiles: IHL-5
+    datagrams start with floor4(start) 4..20 bytes before a 4 KiB and an 8 KiB tile
+    boundary of their chunk (rxgen.tile_edge_batch), at every start alignment."""
+    import rxgen
+    assert batch.ragged_variant("tx_datagram", npk) == kern
+    chunk = 16 if "c16" in kern else 64
+    rng = np.random.default_rng(9600 + npk)
+    special = lambda r, total: rxgen.tx_packet(r, max(0, total - 20), ihl=5)  # noqa: E731
+    for base_off in (0, 1, 2, 3):
+        blob, offs = rxgen.tile_edge_batch(rng, npk, chunk, base_off, special=special)
+        for i in range(npk):  # fillers with protocol 6: keep their TCP segments in contract
+            a, e = int(offs[i]), int(offs[i + 1])
+            blob[a:e] = np.frombuffer(bytes(rxgen.tcp_contract(bytearray(blob[a:e].tobytes()))), np.uint8)
+        got = batch.checksum_ragged(_to(dev, blob), _to(dev, offs.view(np.int64)), "tx_datagram").cpu().numpy()
+        want = oracle_c.batch(blob, O.MODE_TX_DATAGRAM, offsets=offs)
+        assert np.array_equal(got, want), (base_off, np.nonzero(got != want)[0][:10])
+        assert (want[0::2] != 0).mean() > 0.9  # in contract: fillers and specials alike
+
+
+@pytest.mark.parametrize("npk", [777, 70000])
+@pytest.mark.parametrize("length", [20, 28, 64, 576, 1500])
+def test_tx_datagram_uniform(dev, oracle_c, length, npk):
+    """Fixed-size outgoing datagrams in uniform slots (stride > length), values and
+    in-place fields."""
+    import rxgen
+    rng = np.random.default_rng(9700 + length + npk)
+    n, stride = npk, (length + 7) // 4 * 4
+    host = np.zeros(n * stride + 64, np.uint8)
+    for p in range(n if n < 5000 else 3000):
+        pk = bytes(rxgen.tx_packet(rng, length - 20, ihl=5))[:length].ljust(length, b"\0")
+        host[p * stride: p * stride + length] = np.frombuffer(pk, np.uint8)
+    if n >= 5000:  # replicate the first 3000 slots
+        reps = -(-n // 3000)
+        host[: n * stride] = np.tile(host[: 3000 * stride], reps)[: n * stride]
+    want = oracle_c.batch(host, O.MODE_TX_DATAGRAM, stride=stride, length=length, n=n)
+    d = _to(dev, host)
+    got = batch.checksum_uniform(d, stride, length, n, "tx_datagram").cpu().numpy()
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    got = batch.checksum_uniform(d, stride, length, n, "tx_datagram", fill=True).cpu().numpy()
+    assert np.array_equal(got, want)
+    exp = _tx_expected(host, np.arange(n + 1, dtype=np.uint64) * stride, want, length=length)
+    filled = d.cpu().numpy()
+    # slot i = [i*stride, i*stride+length): the gap bytes after each datagram stay
+    assert np.array_equal(filled, exp[0])
+
+
+def test_tx_datagram_host_paths(dev, oracle_c):
+    """TX_DATAGRAM through the host entry points (direct burst, pipelined slices, the
+    scatter-gather form) with fill: two results per packet, fields in host memory."""
+    import rxgen
+    rng = np.random.default_rng(9800)
+    for n in (64, 30000):
+        blob, offs = rxgen.tx_batch(rng, n, lo=0, hi=1480, bad=0.1, pad4=True)
+        want = oracle_c.batch(blob, O.MODE_TX_DATAGRAM, offsets=offs)
+        got = batch.checksum_host_ragged(blob, offs, "tx_datagram")
+        assert np.array_equal(got, want), n
+        buf = blob.copy()
+        got = batch.checksum_host_ragged(buf, offs, "tx_datagram", fill=True)
+        assert np.array_equal(got, want)
+        assert np.array_equal(buf, _tx_expected(blob, offs, want)[0])
+        pk = [bytearray(blob[int(offs[i]):int(offs[i + 1])].tobytes()) for i in range(n)]
+        views = [[np.frombuffer(p, np.uint8)[:7].copy(), np.frombuffer(p, np.uint8)[7:].copy()] for p in pk]
+        got = batch.checksum_host_iov(views, "tx_datagram", fill=True)
+        assert np.array_equal(got, want)
+        joined = np.concatenate([np.concatenate(v) for v in views])
+        assert np.array_equal(joined, _tx_expected(blob, offs, want)[0])
+
+
 @pytest.mark.parametrize("npk", [777, 5000])
 @pytest.mark.parametrize("length", [20, 40, 64, 576, 1500])
 def test_verify_rx_uniform(dev, oracle_c, length, npk):

@@ -247,11 +247,11 @@ def refexec_mode_batch(vecs, mode):
     side = [bytes.fromhex(v["addrs"]) for v in vecs]
     addrs = np.frombuffer(b"".join(side), np.uint8).copy() if mode in (1, 2, 6, 7) else None
     init = np.array([int.from_bytes(s[:2], "little") for s in side], np.uint16) if mode == 0 else None
-    return data, offs, addrs, init, np.array([v["want"] for v in vecs], np.uint16)
+    return data, offs, addrs, init, np.array([v["want"] for v in vecs], np.uint16).reshape(-1)
 
 
 def test_refexec_batch_modes(refexec, oracle_c):
-    assert set(refexec["modes"]) == {str(m) for m in range(9)}
+    assert set(refexec["modes"]) == {str(m) for m in range(10)}
     for mode, vecs in refexec["modes"].items():
         m = int(mode)
         data, offs, addrs, init, want = refexec_mode_batch(vecs, m)
@@ -277,6 +277,32 @@ def test_refexec_provenance(refexec):
         assert ~it.method("header", G.from_bytes(bytes(b), "IPv4"), "CalculateChecksum").v & 0xFFFF == v["want"]
 
 
+def test_tx_datagram_oracle_matches_single_field_modes(oracle_c):
+    """TX_DATAGRAM is the IPV4 field plus the transport mode on b[HL:TL] with the
+    header's addresses; on datagrams built like the reference's senders (fields
+    already set) it reproduces both stored fields, and out-of-contract datagrams
+    give (0, 0)."""
+    import rxgen
+    rng = np.random.default_rng(909)
+    for _ in range(300):
+        pk = bytes(rxgen.make_packet(rng, int(rng.integers(0, 300)), proto=int(rng.choice([1, 6, 17, 47]))))
+        ip, l4 = O.tx_datagram(pk)
+        assert ip == (pk[10] << 8 | pk[11])
+        hl = (pk[0] & 0xF) * 4
+        f = {17: 6, 6: 16, 1: 2}.get(pk[9])
+        assert l4 == (0 if f is None else (pk[hl + f] << 8 | pk[hl + f + 1]))
+        got = oracle_c.batch(np.frombuffer(pk, np.uint8), O.MODE_TX_DATAGRAM, stride=len(pk), length=len(pk), n=1)
+        assert list(got) == [ip, l4]
+    pk = bytearray(rxgen.make_packet(rng, 40, proto=17, ihl=5))
+    for bad in (lambda b: b.__setitem__(0, 0x44),          # IHL 4
+                lambda b: b.__setitem__(slice(2, 4), b"\xff\xff"),  # TotalLength > len
+                lambda b: b.__setitem__(slice(2, 4), b"\x00\x10")):  # TotalLength < HeaderLength
+        b = bytearray(pk)
+        bad(b)
+        assert O.tx_datagram(bytes(b)) == (0, 0)
+    assert O.tx_datagram(bytes(pk[:19])) == (0, 0)
+
+
 @pytest.mark.skipif(" avx2" not in open("/proc/cpuinfo").read(), reason="needs AVX2")
 def test_vectorised_build_agrees(oracle_c):
     """The -O3 -march=x86-64-v3 build (bench's "optimised CPU" baseline) computes the
@@ -289,7 +315,7 @@ def test_vectorised_build_agrees(oracle_c):
     data = rng.integers(0, 256, size=int(offs[-1]) + 8, dtype=np.uint8)
     data[offs[:-1].astype(np.int64) + 12] = rng.integers(5, 16, size=lens.size) << 4  # DataOffset 20..60
     addrs = rng.integers(0, 256, size=8 * lens.size, dtype=np.uint8)
-    for mode in range(9):
+    for mode in range(10):
         a = oracle_c.batch(data, mode, offsets=offs, addrs=addrs)
         b = opt.batch(data, mode, offsets=offs, addrs=addrs, threads=4)
         assert np.array_equal(a, b), mode

@@ -32,7 +32,7 @@ def short_name(full):
     if k == "k_loop":
         return f"k_loop<{args[0]},{'BE' if args[2] == 'true' else 'LE'}>"
     if k == "k_seg":
-        kind = {"2": ",rx", "true": ",rx", "1": ",tx"}.get(args[2], "")  # template K: plain/tx/rx
+        kind = {"2": ",rx", "true": ",rx", "1": ",tx", "3": ",dg"}.get(args[2], "")  # template K: plain/tx/rx/dg
         return f"k_seg<{args[0]}{kind}>"
     if k == "k_rag":
         return f"k_rag<{args[0]},{args[1]}>"
@@ -59,7 +59,7 @@ def main(prof_dir, out_path):
     if os.path.exists(out_path):  # merge: configs not profiled in prof_dir keep their record
         with open(out_path) as f:
             res = json.load(f)
-    for c in ("2", "3", "4", "6", "7", "8", "9", "10"):
+    for c in ("2", "3", "4", "6", "7", "8", "9", "10", "11"):
         cfg = f"config{c}"
         fpath = os.path.join(prof_dir, f"pmc_FETCH_SIZE_c{c}", "run_counter_collection.csv")
         wpath = os.path.join(prof_dir, f"pmc_WRITE_SIZE_c{c}", "run_counter_collection.csv")

@@ -9,7 +9,7 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-for cfg in ${CFGS:-3 2 8 4 6 7 9 10}; do
+for cfg in ${CFGS:-3 2 8 4 6 7 9 10 11}; do
   # 5 warm-up + 30 timed launches; tools/trace_summary.py <csv> 30 averages the same
   # 30 launches bench.py's HIP events time (the stats CSV also counts the warm-up)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_c$cfg" -o run -- \

@@ -21,6 +21,9 @@ VERIFY_UDP     the checker.TCP formula for UDP
 VERIFY_RX      whole received IPv4 packets: IsValid + checker.IPv4 + checker.TCP's
                test, inputs read from each packet; out = YU_RX_* bits
                                                                checker/checker.go:25-99
+TX_DATAGRAM    whole outgoing IPv4 datagrams: both fields (IPv4 header and its
+               sender's transport field), inputs read from each datagram; TWO
+               results per packet, out[2i] / out[2i+1]     network/ipv4/ipv4.go:80-97
 =============  =========================================================================
 """
 from __future__ import annotations
@@ -30,13 +33,13 @@ import torch
 
 from ._lib import check, lib
 
-RAW, UDP, TCP, IPV4, ICMP, VERIFY_IPV4, VERIFY_TCP, VERIFY_UDP, VERIFY_RX = range(9)
+RAW, UDP, TCP, IPV4, ICMP, VERIFY_IPV4, VERIFY_TCP, VERIFY_UDP, VERIFY_RX, TX_DATAGRAM = range(10)
 MODES = {"raw": RAW, "udp": UDP, "tcp": TCP, "ipv4": IPV4, "icmp": ICMP,
          "verify_ipv4": VERIFY_IPV4, "verify_tcp": VERIFY_TCP, "verify_udp": VERIFY_UDP,
-         "verify_rx": VERIFY_RX}
+         "verify_rx": VERIFY_RX, "tx_datagram": TX_DATAGRAM}
 # VERIFY_RX result bits (include/yucsum.h YU_RX_*)
 RX_IP_OK, RX_L4, RX_L4_OK, RX_INVALID = 1, 2, 4, 8
-TX_MODES = (UDP, TCP, IPV4, ICMP)
+TX_MODES = (UDP, TCP, IPV4, ICMP, TX_DATAGRAM)
 MAX_TRANSPORT_LEN = 65535
 MAX_RAW_LEN = 0xFFFF0000  # include/yucsum.h YU_MAX_RAW_LEN
 
@@ -46,6 +49,11 @@ def _mode(m) -> int:
     if not 0 <= m < len(MODES):
         raise ValueError(f"bad mode {m}")
     return m
+
+
+def outputs(mode) -> int:
+    """Results per packet (include/yucsum.h YU_MODE_OUTPUTS): 2 for TX_DATAGRAM."""
+    return 2 if _mode(mode) == TX_DATAGRAM else 1
 
 
 def _dev_u8(t: torch.Tensor, name: str) -> torch.Tensor:
@@ -80,7 +88,7 @@ def checksum_uniform(data: torch.Tensor, stride: int, length: int, n: int, mode=
                      addrs: torch.Tensor | None = None, out: torch.Tensor | None = None,
                      stream: torch.cuda.Stream | None = None, fill: bool = False) -> torch.Tensor:
     """Per-packet sums of a uniform-stride device batch: packet i is
-    ``data[i*stride : i*stride+length]``. Returns a uint16 tensor of n results
+    ``data[i*stride : i*stride+length]``. Returns a uint16 tensor of n results (2n for TX_DATAGRAM)
     (allocated unless ``out`` is given). ``fill=True`` additionally stores each TX
     result big-endian into the packet's checksum field (in place)."""
     m = _mode(mode)
@@ -92,10 +100,11 @@ def checksum_uniform(data: torch.Tensor, stride: int, length: int, n: int, mode=
     dev = data.device
     initial_arr = _opt(initial_arr, torch.uint16, n, dev, "initial_arr")
     addrs = _opt(addrs, torch.uint8, 8 * n, dev, "addrs")
+    k = outputs(m)
     if out is None:
-        out = torch.empty(max(n, 1), dtype=torch.uint16, device=dev)[:n]
+        out = torch.empty(max(n * k, 1), dtype=torch.uint16, device=dev)[:n * k]
     else:
-        _opt(out, torch.uint16, n, dev, "out")
+        _opt(out, torch.uint16, n * k, dev, "out")
     with torch.cuda.device(dev):
         f = lib().yu_csum_fill_uniform if fill else lib().yu_csum_batch_uniform
         rc = f(data.data_ptr(), stride, length, n, m, _ptr(initial_arr), initial & 0xFFFF,
@@ -133,10 +142,11 @@ def checksum_ragged(data: torch.Tensor, offsets: torch.Tensor, mode="raw", *, in
     dev = data.device
     initial_arr = _opt(initial_arr, torch.uint16, n, dev, "initial_arr")
     addrs = _opt(addrs, torch.uint8, 8 * n, dev, "addrs")
+    k = outputs(m)
     if out is None:
-        out = torch.empty(max(n, 1), dtype=torch.uint16, device=dev)[:n]
+        out = torch.empty(max(n * k, 1), dtype=torch.uint16, device=dev)[:n * k]
     else:
-        _opt(out, torch.uint16, n, dev, "out")
+        _opt(out, torch.uint16, n * k, dev, "out")
     with torch.cuda.device(dev):
         f = lib().yu_csum_fill_ragged if fill else lib().yu_csum_batch_ragged
         rc = f(data.data_ptr(), offsets.data_ptr(), n, m, _ptr(initial_arr), initial & 0xFFFF,
@@ -187,11 +197,16 @@ def checksum_host_uniform(data: np.ndarray, stride: int, length: int, n: int, mo
     ad = None if addrs is None else np.ascontiguousarray(addrs, dtype=np.uint8)
     if ia is not None and ia.size < n or ad is not None and ad.size < 8 * n:
         raise ValueError("side arrays too small")
+    k = outputs(m)
     if out is None:
-        out = np.empty(n, dtype=np.uint16)
+        out = np.empty(n * k, dtype=np.uint16)
     if isinstance(out, torch.Tensor):
+        if out.element_size() != 2 or out.is_cuda or not out.is_contiguous() or out.numel() < n * k:
+            raise ValueError("out must be a contiguous 16-bit CPU tensor of >= n results")
         optr = out.data_ptr()
     else:
+        if out.dtype.itemsize != 2 or out.size < n * k or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous 16-bit array of >= n results")
         optr = out.ctypes.data
     args = (dptr, stride, length, n, m, None if ia is None else ia.ctypes.data, initial & 0xFFFF,
             None if ad is None else ad.ctypes.data, optr)
@@ -212,15 +227,15 @@ def _host_call(name: str, args: tuple, device) -> None:
         check(getattr(lib(), name)(*args, int(device)), name)
 
 
-def _host_side(n, initial_arr, addrs, out):
+def _host_side(n, initial_arr, addrs, out, k=1):
     ia = None if initial_arr is None else np.ascontiguousarray(initial_arr, dtype=np.uint16)
     ad = None if addrs is None else np.ascontiguousarray(addrs, dtype=np.uint8)
     if ia is not None and ia.size < n or ad is not None and ad.size < 8 * n:
         raise ValueError("side arrays too small")
     if out is None:
-        out = np.empty(n, dtype=np.uint16)
-    elif out.dtype != np.uint16 or out.size < n or not out.flags.c_contiguous:
-        raise ValueError("out must be a contiguous uint16 array of >= n elements")
+        out = np.empty(n * k, dtype=np.uint16)
+    elif out.dtype != np.uint16 or out.size < n * k or not out.flags.c_contiguous:
+        raise ValueError("out must be a contiguous uint16 array of >= n results")
     return ia, ad, out
 
 
@@ -238,7 +253,7 @@ def checksum_host_ragged(data, offsets, mode="raw", *, initial: int = 0, initial
         raise ValueError("offsets must hold n+1 entries")
     if n and int(offs[-1]) > dlen:
         raise ValueError("offsets run past data")
-    ia, ad, out = _host_side(n, initial_arr, addrs, out)
+    ia, ad, out = _host_side(n, initial_arr, addrs, out, outputs(m))
     args = (dptr, offs.ctypes.data, n, m, None if ia is None else ia.ctypes.data, initial & 0xFFFF,
             None if ad is None else ad.ctypes.data, out.ctypes.data)
     _host_call(_fill_name("yu_csum_batch_host_ragged", fill, device), args, device)
@@ -272,7 +287,7 @@ def checksum_host_iov(packets, mode="raw", *, initial: int = 0, initial_arr=None
             views.append((a.ctypes.data if a.size else None, a.size))
         first[i + 1] = len(views)
     iov = (YuIovec * max(1, len(views)))(*[YuIovec(b, l) for b, l in views])
-    ia, ad, out = _host_side(n, initial_arr, addrs, out)
+    ia, ad, out = _host_side(n, initial_arr, addrs, out, outputs(m))
     args = (ctypes_addr(iov), first.ctypes.data, n, m, None if ia is None else ia.ctypes.data,
             initial & 0xFFFF, None if ad is None else ad.ctypes.data, out.ctypes.data)
     _host_call(_fill_name("yu_csum_batch_host_iov", fill, device), args, device)

@@ -69,7 +69,7 @@ struct Slot {
   uint16_t *h_outc = nullptr;
   uint32_t *h_flag = nullptr;
   uint32_t seq = 0;
-  uint64_t first = 0, cnt = 0;
+  uint64_t first = 0, cnt = 0, outs = 1;  // outs: results per packet
   bool busy = false, staged_out = false;
 };
 
@@ -113,15 +113,16 @@ struct Ctx {
       YU_TRY(hipHostMalloc((void **)&x.h_data, data_bytes ? data_bytes : 16, 0));
       YU_TRY(hipHostMalloc((void **)&x.h_addrs, pk * 8, 0));
       YU_TRY(hipHostMalloc((void **)&x.h_init, pk * 2, 0));
-      YU_TRY(hipHostMalloc((void **)&x.h_out, pk * 2, 0));
+      // results: up to 2 per packet (YU_MODE_OUTPUTS)
+      YU_TRY(hipHostMalloc((void **)&x.h_out, pk * 4, 0));
       YU_TRY(hipHostMalloc((void **)&x.h_off, (pk + 1) * 8, 0));
-      YU_TRY(hipHostMalloc((void **)&x.h_outc, pk * 2, hipHostMallocCoherent));
+      YU_TRY(hipHostMalloc((void **)&x.h_outc, pk * 4, hipHostMallocCoherent));
       YU_TRY(hipHostMalloc((void **)&x.h_flag, 64, hipHostMallocCoherent));
       *x.h_flag = 0;
       YU_TRY(hipMalloc((void **)&x.d_data, data_bytes ? data_bytes : 16));
       YU_TRY(hipMalloc((void **)&x.d_addrs, pk * 8));
       YU_TRY(hipMalloc((void **)&x.d_init, pk * 2));
-      YU_TRY(hipMalloc((void **)&x.d_out, pk * 2));
+      YU_TRY(hipMalloc((void **)&x.d_out, pk * 4));
       YU_TRY(hipMalloc((void **)&x.d_off, (pk + 1) * 8));
     }
     cap_data = data_bytes;
@@ -238,7 +239,7 @@ bool is_pinned(const void *p) {
 int finish(Slot &x, uint16_t *h_out) {
   if (!x.busy) return YU_OK;
   YU_TRY(hipEventSynchronize(x.done));
-  if (x.staged_out) memcpy(h_out + x.first, x.h_out, x.cnt * 2);
+  if (x.staged_out) memcpy(h_out + x.first * x.outs, x.h_out, x.cnt * 2 * x.outs);
   x.busy = false;
   return YU_OK;
 }
@@ -331,7 +332,7 @@ int direct(Slot &x, const Layout &L, uint64_t n, const uint16_t *h_init,
   if (rc) return rc;
   rc = wait_flag(x, seq);
   if (rc) return rc;
-  memcpy(h_out, x.h_outc, n * 2);
+  memcpy(h_out, x.h_outc, n * 2 * YU_MODE_OUTPUTS(L.mode));
   return YU_OK;
 }
 
@@ -404,8 +405,10 @@ int run_slices(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
     rc = L.launch(x.d_data, x.d_off, cnt, d_init, d_addrs, x.d_out, x.st);
     if (rc) return rc;
     x.staged_out = !pin_out;
-    YU_TRY(hipMemcpyAsync(pin_out ? h_out + first : x.h_out, x.d_out, cnt * 2,
+    const uint64_t k = YU_MODE_OUTPUTS(L.mode);
+    YU_TRY(hipMemcpyAsync(pin_out ? h_out + first * k : x.h_out, x.d_out, cnt * 2 * k,
                           hipMemcpyDeviceToHost, x.st));
+    x.outs = k;
     YU_TRY(hipEventRecord(x.done, x.st));
     x.first = first;
     x.cnt = cnt;
@@ -765,7 +768,7 @@ extern "C" int yu_csum_batch_host_uniform_multi(const uint8_t *h_data, uint64_t 
   return fan_out(devices, ndev, even_bounds(n, ndev), [&](int i, uint64_t a, uint64_t cnt) {
     return yu_csum_batch_host_uniform(h_data ? h_data + a * stride : nullptr, stride, len, cnt,
                                       mode, h_initial_arr ? h_initial_arr + a : nullptr, initial,
-                                      h_addrs ? h_addrs + 8 * a : nullptr, h_out + a, devices[i]);
+                                      h_addrs ? h_addrs + 8 * a : nullptr, h_out + a * YU_MODE_OUTPUTS(mode), devices[i]);
   });
 }
 
@@ -785,7 +788,7 @@ extern "C" int yu_csum_batch_host_ragged_multi(const uint8_t *h_data,
                    return yu_csum_batch_host_ragged(
                        h_data, h_offsets + a, cnt, mode,
                        h_initial_arr ? h_initial_arr + a : nullptr, initial,
-                       h_addrs ? h_addrs + 8 * a : nullptr, h_out + a, devices[i]);
+                       h_addrs ? h_addrs + 8 * a : nullptr, h_out + a * YU_MODE_OUTPUTS(mode), devices[i]);
                  });
 }
 
@@ -802,7 +805,7 @@ extern "C" int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t 
   return fan_out(devices, ndev, even_bounds(n, ndev), [&](int i, uint64_t a, uint64_t cnt) {
     return yu_csum_batch_host_iov(iov, first_iov + a, cnt, mode,
                                   h_initial_arr ? h_initial_arr + a : nullptr, initial,
-                                  h_addrs ? h_addrs + 8 * a : nullptr, h_out + a, devices[i]);
+                                  h_addrs ? h_addrs + 8 * a : nullptr, h_out + a * YU_MODE_OUTPUTS(mode), devices[i]);
   });
 }
 
@@ -820,7 +823,8 @@ extern "C" int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t 
 namespace {
 
 bool tx_mode(int m) {
-  return m == YU_MODE_UDP || m == YU_MODE_TCP || m == YU_MODE_IPV4 || m == YU_MODE_ICMP;
+  return m == YU_MODE_UDP || m == YU_MODE_TCP || m == YU_MODE_IPV4 || m == YU_MODE_ICMP ||
+         m == YU_MODE_TX_DATAGRAM;
 }
 
 uint32_t field_offset(int m) {
@@ -835,17 +839,43 @@ uint32_t field_offset(int m) {
 // Byte k of packet i, through a layout's accessor (nullptr past the packet).
 // set(i) writes packet i's field; the packets are split over the copy pool.
 template <class At>
+void put_field(const At &at, uint64_t i, uint32_t f, uint16_t v) {
+  uint8_t *hi = at(i, f), *lo = at(i, f + 1);
+  if (!hi || !lo) return;
+  *hi = (uint8_t)(v >> 8);
+  *lo = (uint8_t)v;
+}
+
+// TX_DATAGRAM: both fields of datagram i where the device defined them
+// (include/yucsum.h): the contract 20 <= HeaderLength() <= TotalLength() <=
+// len read from the bytes, the transport field when the protocol has one and
+// the segment holds its header — the rule the kernels apply.
+template <class At>
+void put_datagram_fields(const At &at, uint64_t i, const uint16_t *res) {
+  const uint8_t *b0 = at(i, 0), *b2 = at(i, 2), *b3 = at(i, 3), *b9 = at(i, 9);
+  if (!at(i, 19)) return;  // shorter than 20 bytes
+  const uint32_t hl = (uint32_t)(*b0 & 0xFu) * 4u, tl = (uint32_t)*b2 << 8 | *b3;
+  if (hl < 20u || hl > tl || !at(i, tl - 1u)) return;
+  put_field(at, i, 10, res[2 * i]);
+  const uint32_t proto = *b9;
+  const uint32_t fo = proto == 17 ? 6 : (proto == 6 ? 16 : (proto == 1 ? 2 : 0));
+  const uint32_t mn = proto == 17 ? 8 : (proto == 6 ? 20 : 4);
+  if (fo && tl - hl >= mn) put_field(at, i, hl + fo, res[2 * i + 1]);
+}
+
+template <class At>
 void set_fields(uint64_t n, int mode, const uint16_t *res, const At &at) {
   const uint32_t f = field_offset(mode);
   auto one = [&](uint64_t i) {
-    uint8_t *hi = at(i, f), *lo = at(i, f + 1);
-    if (!hi || !lo) return;
+    if (mode == YU_MODE_TX_DATAGRAM) {
+      put_datagram_fields(at, i, res);
+      return;
+    }
     if (mode == YU_MODE_IPV4) {  // the field must lie inside the header
       const uint8_t *b0 = at(i, 0);
       if (!b0 || (uint32_t)(*b0 & 0xFu) * 4u < f + 2u) return;
     }
-    *hi = (uint8_t)(res[i] >> 8);
-    *lo = (uint8_t)res[i];
+    put_field(at, i, f, res[i]);
   };
   constexpr uint64_t kParMin = 1u << 16;
   CopyPool &pool = CopyPool::get();
@@ -864,7 +894,7 @@ void set_fields(uint64_t n, int mode, const uint16_t *res, const At &at) {
 struct ResultBuf {
   std::vector<uint16_t> tmp;
   uint16_t *p;
-  ResultBuf(uint16_t *out, uint64_t n) : p(out) {
+  ResultBuf(uint16_t *out, uint64_t n) : p(out) {  // n = results, not packets
     if (!p) {
       tmp.resize(n ? n : 1);
       p = tmp.data();
@@ -880,7 +910,7 @@ extern "C" int yu_csum_fill_host_uniform(uint8_t *h_data, uint64_t stride, uint3
                                          uint16_t *h_out, int device) {
   if (!tx_mode(mode)) return YU_EINVAL;
   if (n == 0) return YU_OK;
-  ResultBuf r(h_out, n);
+  ResultBuf r(h_out, n * YU_MODE_OUTPUTS(mode));
   int rc = yu_csum_batch_host_uniform(h_data, stride, len, n, mode, h_initial_arr, initial,
                                       h_addrs, r.p, device);
   if (rc) return rc;
@@ -896,7 +926,7 @@ extern "C" int yu_csum_fill_host_ragged(uint8_t *h_data, const uint64_t *h_offse
                                         uint16_t *h_out, int device) {
   if (!tx_mode(mode)) return YU_EINVAL;
   if (n == 0) return YU_OK;
-  ResultBuf r(h_out, n);
+  ResultBuf r(h_out, n * YU_MODE_OUTPUTS(mode));
   int rc = yu_csum_batch_host_ragged(h_data, h_offsets, n, mode, h_initial_arr, initial, h_addrs,
                                      r.p, device);
   if (rc) return rc;
@@ -911,7 +941,7 @@ extern "C" int yu_csum_fill_host_iov(const yu_iovec *iov, const uint64_t *first_
                                      const uint8_t *h_addrs, uint16_t *h_out, int device) {
   if (!tx_mode(mode)) return YU_EINVAL;
   if (n == 0) return YU_OK;
-  ResultBuf r(h_out, n);
+  ResultBuf r(h_out, n * YU_MODE_OUTPUTS(mode));
   int rc = yu_csum_batch_host_iov(iov, first_iov, n, mode, h_initial_arr, initial, h_addrs, r.p,
                                   device);
   if (rc) return rc;

@@ -112,6 +112,23 @@ __host__ __device__ __forceinline__ bool mode_is_tx(int m) {
   return m == YU_MODE_UDP || m == YU_MODE_TCP || m == YU_MODE_IPV4 ||
          m == YU_MODE_ICMP;
 }
+// Modes that may write in place (the single-field TX modes and TX_DATAGRAM).
+__host__ __device__ __forceinline__ bool mode_fills(int m) {
+  return mode_is_tx(m) || m == YU_MODE_TX_DATAGRAM;
+}
+// Results per packet in out (include/yucsum.h YU_MODE_OUTPUTS).
+__host__ __device__ __forceinline__ uint32_t mode_outputs(int m) {
+  return m == YU_MODE_TX_DATAGRAM ? 2u : 1u;
+}
+// Offset of the transport checksum field in a segment of IPv4 protocol
+// `proto`, and the segment's minimum length (UDP 6/8, TCP 16/20, ICMP 2/4);
+// 0 / 0 for other protocols.
+__host__ __device__ __forceinline__ uint32_t l4_field(uint32_t proto) {
+  return proto == 17u ? 6u : (proto == 6u ? 16u : (proto == 1u ? 2u : 0u));
+}
+__host__ __device__ __forceinline__ uint32_t l4_min(uint32_t proto) {
+  return proto == 17u ? 8u : (proto == 6u ? 20u : (proto == 1u ? 4u : 0u));
+}
 __host__ __device__ __forceinline__ bool mode_has_pseudo(int m) {
   return m == YU_MODE_UDP || m == YU_MODE_TCP || m == YU_MODE_VERIFY_TCP ||
          m == YU_MODE_VERIFY_UDP;
@@ -1441,7 +1458,35 @@ struct SegRx {
   uint32_t flags;   // YU_RX_* bits known at parse time
   uint32_t pseudo;  // LE-free big-endian word sum of src, dst, proto, length
   uint32_t proto;
+  uint32_t ipf;     // TX_DATAGRAM: LE sum of the IPv4 checksum field's bytes
+  uint32_t hl;      // TX_DATAGRAM: header length (0 outside the contract)
 };
+
+// TX_DATAGRAM on a parsed header (rx_parse): the datagram is in contract when
+// 20 <= HeaderLength() <= TotalLength() <= len; its transport field exists
+// when the protocol is UDP / TCP / ICMP and the segment holds its header.
+// Returns the transport field offset from the packet start (0: none) and
+// records the IPv4 field's bytes (window bytes sh+10, sh+11) for subtraction.
+__device__ __forceinline__ uint32_t dg_parse(SegRx &rx, uint32_t sh, uint32_t hl, uint32_t tl) {
+  const bool ok = !(rx.flags & YU_RX_INVALID) && hl >= 20u;
+  rx.hl = ok ? hl : 0u;
+  uint32_t f = 0;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) f = sad(rx.h[j] & byte_range_mask(4u * (uint32_t)j, sh + 10u, sh + 12u), f);
+  rx.ipf = f;
+  const uint32_t fo = l4_field(rx.proto);
+  return ok && fo && tl - hl >= l4_min(rx.proto) ? hl + fo : 0u;
+}
+
+// A 16-bit field value stored big-endian (binary.BigEndian.PutUint16).
+__device__ __forceinline__ void put_be16(uint8_t *q, uint32_t r) {
+  if (((uintptr_t)q & 1u) == 0) {
+    *(uint16_t *)q = (uint16_t)(((r >> 8) | (r << 8)) & 0xFFFFu);
+  } else {
+    q[0] = (uint8_t)(r >> 8);
+    q[1] = (uint8_t)r;
+  }
+}
 
 // Parse the gathered header of a packet of length len starting sh = start&3
 // bytes into h[0] (header/ipv4.go:91-118,126-138). Returns the header and
@@ -1494,13 +1539,18 @@ __device__ __forceinline__ uint64_t seg_waves(const BatchArgs &A) {
 // Kinds of k_seg by the points a lane evaluates (compile-time, so a kind
 // carries no code or registers for the others): plain (RAW / VERIFY_TCP /
 // VERIFY_UDP: start and end), TX (UDP / TCP / ICMP: + the checksum field's
-// two ends), RX (VERIFY_RX: + header and transport ends).
-constexpr int kSegPlain = 0, kSegTx = 1, kSegRx = 2;
+// two ends), RX (VERIFY_RX: + header and transport ends), DG (TX_DATAGRAM:
+// RX's points + the transport field's two ends; the IPv4 field comes off the
+// parsed header's registers).
+constexpr int kSegPlain = 0, kSegTx = 1, kSegRx = 2, kSegDg = 3;
 
+// (the DG kind asks for at least 3 waves per SIMD: its two extra points would
+// otherwise take it to 170 VGPRs, 2 waves; the other kinds are left alone)
 template <int U, int NT, int K, int CH = 64>
-__global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
-  constexpr bool RX = K == kSegRx;
-  constexpr int NP = K == kSegPlain ? 2 : 4;  // point slots in use
+__global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
+  constexpr bool DG = K == kSegDg;
+  constexpr bool RX = K == kSegRx || DG;  // parses each packet's IPv4 header
+  constexpr int NP = K == kSegPlain ? 2 : (DG ? 6 : 4);  // point slots in use
   constexpr uint32_t T = 64u * 16u * U;
   constexpr uint32_t NC = 64u * U;  // chunks per tile
   __shared__ uint4 s_data[4][NC];   // the tile's bytes
@@ -1527,7 +1577,8 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
   seg_geom(data, A.n, ch * CH, cur);
 
   // per-chunk state
-  SegPt pt[4];  // start, end, then field start/end (TX) or header/transport end (RX)
+  SegPt pt[6];  // start, end, then field start/end (TX) or header/transport end (RX),
+                // then (DG) the transport field's start/end; slots past NP unused
   SegRx rx;
   bool exact = false;
   uint32_t carry_l = 0, carry_t = 0;
@@ -1547,8 +1598,10 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
       rx.need = len >= 20u ? (1u << (((19u + sh) >> 2) + 1u)) - 1u : 0u;
       rx.flags = YU_RX_INVALID;
       rx.pseudo = rx.proto = 0u;
+      rx.ipf = rx.hl = 0u;
 #pragma unroll
       for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
+      if (DG) pt[2].x = pt[3].x = pt[4].x = pt[5].x = kNoPt;
     }
 #pragma unroll
     for (int i = 0; i < NP; ++i) pt[i].p = pt[i].t = 0u;
@@ -1622,8 +1675,22 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
         if (rx.need == 0u) {
           uint32_t hl, tl;
           rx_parse(rx, (uint32_t)pt[0].x & 3u, cur.oy - cur.ox, hl, tl);
-          pt[2].x = pt[0].x + hl;
-          pt[3].x = pt[0].x + tl;
+          if (DG) {
+            // in contract HeaderLength() >= 20: every point lies at or past
+            // byte 20, so never in a tile that has gone by
+            const uint32_t fo = dg_parse(rx, (uint32_t)pt[0].x & 3u, hl, tl);
+            if (rx.hl) {
+              pt[2].x = pt[0].x + hl;
+              pt[3].x = pt[0].x + tl;
+            }
+            if (fo) {
+              pt[4].x = pt[0].x + fo;
+              pt[5].x = pt[0].x + fo + 2u;
+            }
+          } else {
+            pt[2].x = pt[0].x + hl;
+            pt[3].x = pt[0].x + tl;
+          }
           parsed = true;
         }
       }
@@ -1635,7 +1702,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
           pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
         }
       }
-      if (RX && parsed) {
+      if (RX && !DG && parsed) {
         // A header straddling two tiles is parsed in the second, but a header
         // or total length under 20 bytes (IsValid accepts IHL 0..4) can put
         // its point in the first, whose bytes have gone by. Such a point lies
@@ -1693,7 +1760,26 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
     const uint64_t p = ch * CH + lane;
     if (lane < (uint32_t)CH && p < A.n) {
       const uint32_t odd = (uint32_t)pt[0].x & 1u;
-      if (RX) {
+      if (DG) {
+        // IPv4 header field: ^Checksum(b[:HeaderLength()]) with the field as 0
+        // (network/ipv4/ipv4.go:85-94); transport field: the sender's value
+        // over b[HeaderLength():TotalLength()] with its field as 0 and the
+        // pseudo header + length from the datagram (sendUDP / sendTCP /
+        // sendICMPv4, see include/yucsum.h)
+        uint32_t ip = 0u, l4 = 0u;
+        if (rx.hl) ip = ~fold32(le_to_be(pt[2].p - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
+        const bool has_l4 = pt[4].x != kNoPt;
+        if (has_l4)
+          l4 = ~fold32(le_to_be(pt[3].p - pt[2].p - (pt[5].p - pt[4].p), odd) + rx.pseudo) & 0xFFFFu;
+        if (A.out) {
+          A.out[2u * p] = (uint16_t)ip;
+          A.out[2u * p + 1u] = (uint16_t)l4;
+        }
+        if (A.fill) {
+          if (rx.hl) put_be16(A.fill + cur.ox + 10u, ip);
+          if (has_l4) put_be16(A.fill + cur.ox + (pt[4].x - pt[0].x), l4);
+        }
+      } else if (RX) {
         // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
         // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
         uint32_t r = rx.flags;
@@ -1749,7 +1835,7 @@ __global__ __launch_bounds__(256) void k_seg(BatchArgs A) {
 // sum [sh+hl, sh+tl) through byte masks (window coordinates, base floor4 of
 // the start). Same checks and result bits as k_seg's RX kind.
 // ---------------------------------------------------------------------
-template <int U, int NT>
+template <int U, int NT, bool DG = false>
 __global__ __launch_bounds__(256) void k_loop_rx(BatchArgs A) {
   constexpr uint32_t W = 64u * 16u * U;
   const uint32_t lane = threadIdx.x & 63u;
@@ -1766,7 +1852,7 @@ __global__ __launch_bounds__(256) void k_loop_rx(BatchArgs A) {
   uint32_t wb = 0;
   uint4 c[U];
   loop_fetch<U, NT>(cur, 0, lane, end, c);
-  uint32_t ah = 0, at = 0, hl = 0, tl = 0;
+  uint32_t ah = 0, at = 0, hl = 0, tl = 0, fo = 0;
   SegRx rx;
   for (;;) {
     const bool last = wb + W >= cur.eload;  // wave-uniform
@@ -1784,8 +1870,16 @@ __global__ __launch_bounds__(256) void k_loop_rx(BatchArgs A) {
       rx.pseudo = 0u;
       hl = tl = 0u;
       if (cur.len >= 20u) rx_parse(rx, cur.sh, cur.len, hl, tl);  // IsValid: minimum size
+      if (DG) {  // TX_DATAGRAM: the two fields come off by byte masks
+        rx.hl = 0u;
+        fo = cur.len >= 20u ? dg_parse(rx, cur.sh, hl, tl) : 0u;
+        if (!rx.hl) hl = tl = 0u;
+      }
     }
     const uint32_t a = cur.sh, b = cur.sh + hl, e = cur.sh + tl;
+    // DG: the IPv4 field [10, 12) and the transport field [fo, fo + 2) are
+    // left out of the header and transport sums (empty ranges when absent)
+    const uint32_t ia = DG && rx.hl ? cur.sh + 10u : 0u, ta = DG && fo ? cur.sh + fo : 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t w[4] = {c[u].x, c[u].y, c[u].z, c[u].w};
@@ -1793,14 +1887,31 @@ __global__ __launch_bounds__(256) void k_loop_rx(BatchArgs A) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t lo = base + 4u * (uint32_t)j;
-        ah = sad(w[j] & byte_range_mask(lo, a, b), ah);
-        at = sad(w[j] & byte_range_mask(lo, b, e), at);
+        if (DG) {
+          ah = sad(w[j] & byte_range_mask(lo, a, b) & ~byte_range_mask(lo, ia, ia + (ia ? 2u : 0u)), ah);
+          at = sad(w[j] & byte_range_mask(lo, b, e) & ~byte_range_mask(lo, ta, ta + (ta ? 2u : 0u)), at);
+        } else {
+          ah = sad(w[j] & byte_range_mask(lo, a, b), ah);
+          at = sad(w[j] & byte_range_mask(lo, b, e), at);
+        }
       }
     }
     if (last) {
       ah = group_total<64>(ah);
       at = group_total<64>(at);
-      if (lane == 63u) {
+      if (DG && lane == 63u) {  // TX_DATAGRAM: as k_seg's DG kind
+        const uint32_t odd = cur.sh & 1u;
+        const uint32_t ip = rx.hl ? ~fold32(le_to_be(ah, odd)) & 0xFFFFu : 0u;
+        const uint32_t l4 = fo ? ~fold32(le_to_be(at, odd) + rx.pseudo) & 0xFFFFu : 0u;
+        if (A.out) {
+          A.out[2u * p] = (uint16_t)ip;
+          A.out[2u * p + 1u] = (uint16_t)l4;
+        }
+        if (A.fill) {
+          if (rx.hl) put_be16(A.fill + cur.soff + 10u, ip);
+          if (fo) put_be16(A.fill + cur.soff + fo, l4);
+        }
+      } else if (lane == 63u) {
         // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
         // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
         uint32_t r = rx.flags;
@@ -1883,6 +1994,8 @@ const Variant kSmall[] = {
 const Variant kLoopLE = {"k_loop<4,LE>", 0, {k_loop<4, 0, false>, k_loop<4, 1, false>, k_loop<4, 1, false>}, 64, 1};
 const Variant kLoopBE = {"k_loop<4,BE>", 0, {k_loop<4, 0, true>, k_loop<4, 1, true>, k_loop<4, 1, true>}, 64, 1};
 const Variant kLoopRx = {"k_loop<4,rx>", 0, {k_loop_rx<4, 0>, k_loop_rx<4, 1>, k_loop_rx<4, 1>}, 64, 1};
+const Variant kLoopDg = {"k_loop<4,dg>", 0,
+                         {k_loop_rx<4, 0, true>, k_loop_rx<4, 1, true>, k_loop_rx<4, 1, true>}, 64, 1};
 const Variant kRag = {"k_rag<16,6>", 1536, {k_rag<16, 6, 0>, k_rag<16, 6, 1>, k_rag<16, 6, 2>}, 16, 4};
 // plain loads by default: for scattered 32-byte header reads they beat nt
 // ones (30.7 vs 32.5 us, kbench 12)
@@ -1901,10 +2014,14 @@ const Variant kSegRx8 = YU_SEG(8, kSegRx, "k_seg<8,rx>");
 const Variant kSeg8c16 = YU_SEG16(8, kSegPlain, "k_seg<8,c16>");
 const Variant kSegTx8c16 = YU_SEG16(8, kSegTx, "k_seg<8,tx,c16>");
 const Variant kSegRx8c16 = YU_SEG16(8, kSegRx, "k_seg<8,rx,c16>");
+// (no 4 KiB-tile DG kind: datagram batches take the ragged picks, 8 KiB)
+const Variant kSegDg8 = YU_SEG(8, kSegDg, "k_seg<8,dg>");
+const Variant kSegDg8c16 = YU_SEG16(8, kSegDg, "k_seg<8,dg,c16>");
 
 // The k_seg kind for a mode (not the IPv4 header-only modes).
 const Variant &seg_for(bool u8, int mode) {
   if (mode == YU_MODE_VERIFY_RX) return u8 ? kSegRx8 : kSegRx4;
+  if (mode == YU_MODE_TX_DATAGRAM) return kSegDg8;
   if (mode_is_tx(mode)) return u8 ? kSegTx8 : kSegTx4;
   return u8 ? kSeg8 : kSeg4;
 }
@@ -1930,17 +2047,19 @@ const Variant &pick_ragged(int mode, uint64_t n) {
   static const char *f = getenv("YU_RAGGED");
   const bool seg4 = f && strcmp(f, "seg4") == 0;
   const bool rx = mode == YU_MODE_VERIFY_RX;  // only k_seg verifies whole datagrams
-  const Variant &loop = rx ? kLoopRx : (mode == YU_MODE_RAW ? kLoopBE : kLoopLE);  // BE: exact past 131072 B
+  const bool dg = mode == YU_MODE_TX_DATAGRAM;  // and fills both fields of one
+  const Variant &loop = rx ? kLoopRx : (dg ? kLoopDg : (mode == YU_MODE_RAW ? kLoopBE : kLoopLE));  // BE: exact past 131072 B
+  const Variant &c16 = rx ? kSegRx8c16 : (dg ? kSegDg8c16 : (mode_is_tx(mode) ? kSegTx8c16 : kSeg8c16));
   if (f && strcmp(f, "loop") == 0) return loop;
-  if (f && strcmp(f, "rag") == 0 && !rx) return kRag;
+  if (f && strcmp(f, "rag") == 0 && !rx && !dg) return kRag;
   if (mode_is_ipv4(mode)) return kHdr;  // header-only: one lane per packet
-  if (f && strcmp(f, "seg16") == 0) return rx ? kSegRx8c16 : (mode_is_tx(mode) ? kSegTx8c16 : kSeg8c16);
+  if (f && strcmp(f, "seg16") == 0) return c16;
   if (n <= kSmallBurst && !f) return loop;
   // up to 64K packets: 16-packet chunks, 4x the waves (U{64..1500}: 8192
   // packets 11.2 -> 6.3 us, 32768 11.7 -> 8.7; U{40..200} 5.1 -> 4.4; jumbo
   // 44.2 -> 17.0; VERIFY_RX 13.3 -> 7.1); from 65536 on 64-packet chunks win
   // again (13.1 vs 14.7 us; profiles/r01/kbench_kseg_chunk16_sweep.log)
-  if (n < kMidBatch && !f) return rx ? kSegRx8c16 : (mode_is_tx(mode) ? kSegTx8c16 : kSeg8c16);
+  if (n < kMidBatch && !f) return c16;
   return seg_for(!seg4, mode);
 }
 
@@ -1962,14 +2081,15 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
     return span <= v.window && v.ppw * stride + v.window < kOOB;
   };
   // k_tiny: no junk bytes (4-aligned starts, no TX field, no IPv4 header walk)
-  const bool tiny_ok = aligned4 && !mode_is_ipv4(mode) && mode != YU_MODE_VERIFY_RX;
+  const bool tiny_ok = aligned4 && !mode_is_ipv4(mode) && mode != YU_MODE_VERIFY_RX &&
+                       mode != YU_MODE_TX_DATAGRAM;
   // k_lane: the same modes, one wave step = 64 whole strides in LDS, so only
   // where gaps between packets waste at most half the bytes it loads
   auto lane_fits = [&](const Variant &v) {
     return tiny_ok && (stride & 3u) == 0 && len >= 1u && len <= stride && stride <= v.window &&
            2u * stride <= 3u * (uint64_t)len;
   };
-  if (mode == YU_MODE_VERIFY_RX) return pick_ragged(mode, n);
+  if (mode == YU_MODE_VERIFY_RX || mode == YU_MODE_TX_DATAGRAM) return pick_ragged(mode, n);
   // IPv4 header-only modes: one lane per packet (1M x 1500-B datagrams:
   // 29.9 us vs 36.9 with k_small<4,1>, kbench 13)
   if (mode_is_ipv4(mode) && !forced_variant()) return kHdr;
@@ -2112,7 +2232,7 @@ int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
                  const uint16_t *out, bool fill) {
   if (mode < 0 || mode >= YU_MODE_COUNT) return YU_EINVAL;
   if (!out && !fill) return YU_EINVAL;
-  if (fill && !mode_is_tx(mode)) return YU_EINVAL;
+  if (fill && !mode_fills(mode)) return YU_EINVAL;
   if (initial_arr && !aligned(initial_arr, 2)) return YU_EINVAL;
   if (addrs && !aligned(addrs, 4)) return YU_EINVAL;
   if (out && !aligned(out, 2)) return YU_EINVAL;
