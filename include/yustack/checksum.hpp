@@ -213,7 +213,11 @@ enum Mode : int {
   VERIFY_TCP = YU_MODE_VERIFY_TCP,
   VERIFY_UDP = YU_MODE_VERIFY_UDP,
   VERIFY_RX = YU_MODE_VERIFY_RX,  // out[i] = YU_RX_* bits
+  TX_DATAGRAM = YU_MODE_TX_DATAGRAM,  // out[2i] = IPv4 field, out[2i+1] = transport field
 };
+
+// Results per packet in `out` (YU_MODE_OUTPUTS): 2 for TX_DATAGRAM, else 1.
+inline constexpr uint64_t Outputs(Mode m) { return YU_MODE_OUTPUTS(m); }
 
 struct Side {
   const uint16_t *initial_arr = nullptr;  // per-packet initial / pseudo partial
