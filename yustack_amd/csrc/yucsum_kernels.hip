@@ -2162,11 +2162,15 @@ int env_int(const char *name, int lo, int hi, int dflt) {
 // what is resident at once (5-8 blocks/CU): finished blocks are replaced by
 // fresh ones, which evens out the per-CU tail. Measured optimum on MI355X
 // (tools/kbench, round 1): 64 for MTU-size and larger packets, 16 for the
-// tiny-packet variants (G < 16).
-int blocks_per_cu(uint32_t G) {
+// small-packet lane-group variants (G < 16). The 64-packet-step kernels
+// (k_lane, k_tiny: `step64`) run best on 6 (round 2, each wave then streams
+// about 4 steps with the next in flight): 1M x 64 B 14.2 -> 13.4 us, 72 B 16.0
+// -> 14.8, 32 B 10.4 -> 8.4, 100 B 21.7 -> 20.8, 124 B 25.0 -> 23.8
+// (profiles/r02/kbench_ab_lane_grid.log).
+int blocks_per_cu(uint32_t G, bool step64) {
   static int v = env_int("YU_BLOCKS_PER_CU", 1, 1024, 0);
   if (v) return v;
-  return G < 16 ? 16 : 64;
+  return step64 ? 6 : (G < 16 ? 16 : 64);
 }
 
 int use_nt() {
@@ -2202,7 +2206,7 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_status(e);
   const uint64_t waves_per_block = 4;
-  const uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu(v.G);
+  const uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu(v.G, is_tiny(v));
   // k_small: runs from 8 runs per CU up (1500-B packets, runs vs interleaved:
   // 16384 packets 8.0 vs 7.2 us, 32768 11.3 vs 12.5, 131072 35.3 vs 38.8; 768-B
   // packets 6.6 vs 5.0, 7.5 vs 8.2, 19.7 vs 22.0; kbench_ab_k_small_runs.log)
