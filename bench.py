@@ -323,6 +323,22 @@ def end_to_end(w: Workload, reps: int = 3):
         for _ in range(k):
             batch.checksum_host_ragged(blob, offs, "verify_rx", out=o)
         res[f"rx_burst{bn}_pinned_us_per_call"] = round((time.perf_counter() - t0) / k * 1e6, 1)
+    # tun TX bursts: whole outgoing TCP/IPv4 datagrams U{40..1500} B (IHL 5, DataOffset
+    # 5) in pinned memory, both checksum fields written in place (TX_DATAGRAM fill)
+    for bn in (64, 1024):
+        lens = (rng.integers(40, 1501, size=bn) + 3) & ~3  # 4-aligned offsets (fill contract)
+        offs = np.zeros(bn + 1, np.int64)
+        offs[1:] = np.cumsum(lens)
+        blob = torch.from_numpy(rng.integers(0, 256, size=int(offs[-1]), dtype=np.uint8)).pin_memory()
+        b, s0 = blob.numpy(), offs[:-1]
+        b[s0], b[s0 + 2], b[s0 + 3], b[s0 + 9], b[s0 + 32] = 0x45, lens >> 8, lens & 0xFF, 6, 0x50
+        for _ in range(10):
+            batch.checksum_host_ragged(blob, offs, "tx_datagram", fill=True)
+        k = 300
+        t0 = time.perf_counter()
+        for _ in range(k):
+            batch.checksum_host_ragged(blob, offs, "tx_datagram", fill=True)
+        res[f"tx_burst{bn}_pinned_us_per_call"] = round((time.perf_counter() - t0) / k * 1e6, 1)
     ndev = torch.cuda.device_count()
     if ndev > 1:  # yu_csum_batch_host_uniform_multi: one shard per visible GPU, each on its own PCIe link
         devs = list(range(ndev))

@@ -339,6 +339,40 @@ def test_tx_datagram_ragged(dev, oracle_c, npk):
     assert (rx[l4_def] & (O.RX_L4 | O.RX_L4_OK) == (O.RX_L4 | O.RX_L4_OK)).all()
 
 
+def test_tx_datagram_fuzz(dev, oracle_c):
+    """Seeded TX_DATAGRAM batches of 1 to 70000 datagrams: random sizes (tiny, MTU,
+    jumbo), protocols, IHL 5..15, a share damaged or out of contract, random start
+    alignment (values) and 4-aligned placement (in place, where only the defined
+    fields may change). YU_TX_FUZZ_SEED / YU_TX_FUZZ_ITERS for longer runs by hand."""
+    import os
+    import rxgen
+    rng = np.random.default_rng(int(os.environ.get("YU_TX_FUZZ_SEED", "5151")))
+    sizes = [1, 2, 63, 64, 65, 4096, 4097, 65535, 65536, 70000]
+    seen = set()
+    for it in range(int(os.environ.get("YU_TX_FUZZ_ITERS", "12"))):
+        npk = sizes[it] if it < len(sizes) else int(rng.integers(1, 20000))
+        lo, hi = [(0, 40), (0, 300), (0, 1480), (1000, 9000)][int(rng.integers(0, 4))]
+        if npk > 10000:
+            lo, hi = min(lo, 100), min(hi, 300)
+        blob, offs = rxgen.tx_batch(rng, npk, lo=lo, hi=hi, bad=float(rng.random()) * 0.5, pad4=True)
+        seen.add(batch.ragged_variant("tx_datagram", npk))
+        want = oracle_c.batch(blob, O.MODE_TX_DATAGRAM, offsets=offs)
+        base_off = int(rng.integers(0, 16))
+        b = np.concatenate([np.zeros(base_off, np.uint8), blob, np.zeros(32, np.uint8)])
+        got = batch.checksum_ragged(_to(dev, b), _to(dev, (offs + base_off).view(np.int64)),
+                                    "tx_datagram").cpu().numpy()
+        assert np.array_equal(got, want), (it, npk, lo, hi, base_off, np.nonzero(got != want)[0][:10])
+        pad = 4 * int(rng.integers(0, 4))
+        d = _to(dev, np.concatenate([np.zeros(pad, np.uint8), blob, np.zeros(32, np.uint8)]))
+        got = batch.checksum_ragged(d, _to(dev, (offs + pad).view(np.int64)), "tx_datagram",
+                                    fill=True).cpu().numpy()
+        assert np.array_equal(got, want), (it, npk, "fill")
+        filled = d.cpu().numpy()[pad:pad + blob.size]
+        assert np.array_equal(filled, _tx_expected(blob, offs, want)[0]), (it, npk, "fill bytes")
+    if int(os.environ.get("YU_TX_FUZZ_ITERS", "12")) >= len(sizes) and not os.environ.get("YU_RAGGED"):
+        assert {"k_loop<4,dg>", "k_seg<8,dg,c16>", "k_seg<8,dg>"} <= seen, seen
+
+
 @pytest.mark.parametrize("npk,kern", [(5000, "k_seg<8,dg,c16>"), (66000, "k_seg<8,dg>")])
 def test_tx_datagram_header_straddles_tile(dev, oracle_c, npk, kern):
     """k_seg's DG kind gathers each datagram's first 20 header bytes across tiles: IHL-5
