@@ -713,6 +713,12 @@ def test_host_multi_device_paths(dev, oracle_c):
         pkts = [[rblob[int(roffs[i]):int(roffs[i + 1])]] for i in range(roffs.size - 1)]
         got = batch.checksum_host_iov(pkts, "verify_rx", device=devs)
         assert np.array_equal(got, oracle_c.batch(rblob, O.MODE_VERIFY_RX, offsets=roffs)), devs
+        # two results per packet: each shard's results land at 2 x its first packet
+        tblob, toffs = rxgen.tx_batch(rng, 3001, lo=0, hi=1480)
+        want = oracle_c.batch(tblob, O.MODE_TX_DATAGRAM, offsets=toffs)
+        assert np.array_equal(batch.checksum_host_ragged(tblob, toffs, "tx_datagram", device=devs), want), devs
+        tpk = [[tblob[int(toffs[i]):int(toffs[i + 1])]] for i in range(toffs.size - 1)]
+        assert np.array_equal(batch.checksum_host_iov(tpk, "tx_datagram", device=devs), want), devs
     # more shards than packets: empty shards are skipped
     host = _rand(rng, 3 * 64)
     got = batch.checksum_host_uniform(host, 64, 64, 3, "raw", device=[0] * 5)
