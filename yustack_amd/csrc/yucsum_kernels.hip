@@ -532,9 +532,21 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
   if (pb >= A.n) return;
   uint32_t res = 0;  // PR: lane s < PR collects the run's result s
   Side rs, nrs;      // PR: the current / next run's side record of packet `lane`
+  // Where a run's side records sit. G <= 16 (a group within one DPP row): the
+  // record of step j for group g is loaded by the group's lane G-1-j, so the
+  // group's last lane, which finishes the packet, holds step 0's and a row_shr:1
+  // after each step brings the next one to it (no LDS permute). G > 16: lane s
+  // loads the run's record s, fetched with a permute each step.
+  constexpr bool kDppSide = G <= 16;
   auto run_side = [&](uint64_t q, Side &d) __attribute__((always_inline)) {
-    const uint64_t x = q + lane;  // lanes >= PR read the run's first record again
-    d = load_side(sp, lane < (uint32_t)PR && x < A.n ? x : (q < A.n ? q : A.n - 1));
+    uint64_t x = q + lane;  // lanes >= PR read the run's first record again
+    bool own = lane < (uint32_t)PR;
+    if (kDppSide) {
+      const uint32_t jj = (uint32_t)(G - 1) - gl;  // step whose record this lane holds
+      x = q + (uint64_t)jj * GPW + gw;
+      own = jj < (uint32_t)SPR;
+    }
+    d = load_side(sp, own && x < A.n ? x : (q < A.n ? q : A.n - 1));
   };
   // One step: issue the loads of the next step into `nx`, then sum `it` and
   // finish its packets. Returns false when the wave has no next step. The
@@ -565,11 +577,21 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
       else
         acc = sum_masked<false>(it.c[u], cr, lim, tm, 0u, acc);
     }
-    acc = group_total<G>(acc);
     const uint64_t p = pb + gw;
     const Junk j = make_junk(it.sh, E, mode);
-    uint32_t jx[3];
-    junk_take<__builtin_ctz(G)>(it.c[0], lane & ~(uint32_t)(G - 1), j, jx);
+    uint32_t jx[3] = {0u, 0u, 0u};
+    if (PR && kDppSide) {
+      // the junk dwords lie in step 0's chunks of the group's first lanes: each
+      // lane takes its own share off its partial sum before the reduction
+      uint32_t own = 0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if ((j.off[i] >> 4) == gl) own = sad(pick_dword(it.c[0], (j.off[i] >> 2) & 3u) & j.mask[i], own);
+      acc -= own;
+    } else {
+      junk_take<__builtin_ctz(G)>(it.c[0], lane & ~(uint32_t)(G - 1), j, jx);
+    }
+    acc = group_total<G>(acc);
     if (PR == 0) {
       if (gl == G - 1 && p < A.n) {
         const uint32_t v = le_to_be(acc - junk_sum<false>(jx, j, 0u), it.sh & 1u);
@@ -577,14 +599,22 @@ __global__ __launch_bounds__(256) void k_small(BatchArgs A) {
                       A.fill ? A.fill + p * A.stride : nullptr, E - it.sh);
       }
     } else {
-      // the group's side record, from the lane that loaded it for the run
-      const int src = (int)(k * GPW + gw);
+      // the group's side record: in its last lane (G <= 16, then shifted on for
+      // the next step), else from the lane that loaded it for the run
       Side sd;
-      sd.a = (uint32_t)__shfl((int)rs.a, src, 64);
-      sd.b = (uint32_t)__shfl((int)rs.b, src, 64);
-      sd.i = (uint16_t)__shfl((int)rs.i, src, 64);
+      if (kDppSide) {
+        sd = rs;
+        rs.a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rs.a, 0x111, 0xf, 0xf, true);  // row_shr:1
+        rs.b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rs.b, 0x111, 0xf, 0xf, true);
+        rs.i = (uint16_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)rs.i, 0x111, 0xf, 0xf, true);
+      } else {
+        const int src = (int)(k * GPW + gw);
+        sd.a = (uint32_t)__shfl((int)rs.a, src, 64);
+        sd.b = (uint32_t)__shfl((int)rs.b, src, 64);
+        sd.i = (uint16_t)__shfl((int)rs.i, src, 64);
+      }
       // every lane computes; the group's last lane holds the true value
-      const uint32_t v = le_to_be(acc - junk_sum<false>(jx, j, 0u), it.sh & 1u);
+      const uint32_t v = le_to_be(acc - (kDppSide ? 0u : junk_sum<false>(jx, j, 0u)), it.sh & 1u);
       const uint32_t r = packet_value(A, v, it.len, sd);
       if (gl == G - 1 && p < A.n && A.fill) store_field(A, r, A.fill + p * A.stride, E - it.sh);
       const uint32_t got = (uint32_t)__shfl((int)r, (int)((lane % GPW) * G + G - 1), 64);
