@@ -339,6 +339,36 @@ def test_tx_datagram_ragged(dev, oracle_c, npk):
     assert (rx[l4_def] & (O.RX_L4 | O.RX_L4_OK) == (O.RX_L4 | O.RX_L4_OK)).all()
 
 
+@pytest.mark.parametrize("npk", [5000, 70000])
+@pytest.mark.parametrize("mode,lo", [(O.MODE_UDP, 8), (O.MODE_TCP, 20), (O.MODE_ICMP, 4)])
+def test_fill_ragged_small_packets_tile_write_back(dev, oracle_c, mode, lo, npk):
+    """In place on ragged small packets: a chunk that fits one 8 KiB tile is written
+    back whole from the patched tile (k_seg<8,tx>); a chunk with a large packet keeps
+    the 2-byte field stores. Only the fields change, chunk edges included (4-aligned
+    offsets, the fill contract), and the results equal the oracle's."""
+    rng = np.random.default_rng(9900 + 7 * mode + npk)
+    lens = (rng.integers(lo, 201, size=npk) + 3) & ~3
+    lens[rng.choice(npk, size=npk // 500, replace=False)] = 4 * rng.integers(1000, 2500, size=npk // 500)
+    offs = np.zeros(npk + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    blob = _rand(rng, int(offs[-1]) + 64)
+    if mode == O.MODE_TCP:
+        blob[offs[:-1].astype(np.int64) + 12] = 0x50
+    addrs = _rand(rng, 8 * npk)
+    want = oracle_c.batch(blob, mode, offsets=offs, addrs=addrs if mode != O.MODE_ICMP else None)
+    d = _to(dev, blob)
+    got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), mode,
+                                addrs=_to(dev, addrs) if mode != O.MODE_ICMP else None, fill=True).cpu().numpy()
+    assert np.array_equal(got, want)
+    f = {O.MODE_UDP: 6, O.MODE_TCP: 16, O.MODE_ICMP: 2}[mode]
+    exp = blob.copy()
+    fi = offs[:-1].astype(np.int64) + f
+    exp[fi] = (want >> 8).astype(np.uint8)
+    exp[fi + 1] = (want & 0xFF).astype(np.uint8)
+    bad = np.nonzero(d.cpu().numpy() != exp)[0]
+    assert bad.size == 0, bad[:10]
+
+
 def test_tx_datagram_fuzz(dev, oracle_c):
     """Seeded TX_DATAGRAM batches of 1 to 70000 datagrams: random sizes (tiny, MTU,
     jumbo), protocols, IHL 5..15, a share damaged or out of contract, random start

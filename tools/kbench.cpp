@@ -98,7 +98,9 @@ int main(int argc, char **argv) {
       std::mt19937_64 rng(4);
       std::uniform_int_distribution<int> d(lo, hi);
       std::vector<uint64_t> off(n + 1, 0);
-      for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + d(rng);
+      // KB_ALIGN4=1: lengths rounded up to 4 (the in-place writer's contract)
+      const bool a4 = getenv("KB_ALIGN4") && atoi(getenv("KB_ALIGN4"));
+      for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + (a4 ? (d(rng) + 3) & ~3 : d(rng));
       bytes = off[n];
       alg = bytes + 8 * (n + 1) + (mode == YU_MODE_RAW ? 4 : 10) * n;
       if (mode == YU_MODE_IPV4) alg = 40 * n + 8 * (n + 1) + 2 * n;  // ~mean IHL*4 of random headers
