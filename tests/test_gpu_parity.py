@@ -341,11 +341,10 @@ def test_tx_datagram_ragged(dev, oracle_c, npk):
 
 @pytest.mark.parametrize("npk", [5000, 70000])
 @pytest.mark.parametrize("mode,lo", [(O.MODE_UDP, 8), (O.MODE_TCP, 20), (O.MODE_ICMP, 4)])
-def test_fill_ragged_small_packets_tile_write_back(dev, oracle_c, mode, lo, npk):
-    """In place on ragged small packets: a chunk that fits one 8 KiB tile is written
-    back whole from the patched tile (k_seg<8,tx>); a chunk with a large packet keeps
-    the 2-byte field stores. Only the fields change, chunk edges included (4-aligned
-    offsets, the fill contract), and the results equal the oracle's."""
+def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk):
+    """In place on ragged small packets (4-aligned offsets, the fill contract) with a
+    few large ones among them, in 16- and 64-packet k_seg chunks: only the fields
+    change, chunk edges included, and the results equal the oracle's."""
     rng = np.random.default_rng(9900 + 7 * mode + npk)
     lens = (rng.integers(lo, 201, size=npk) + 3) & ~3
     lens[rng.choice(npk, size=npk // 500, replace=False)] = 4 * rng.integers(1000, 2500, size=npk // 500)
