@@ -241,6 +241,31 @@ static void test_gpu_batches() {
   batch::FillHostRagged(blank.data(), soff.data(), n, batch::TCP, nullptr, hside);
   EXPECT(blank == segs, "host fill restores every TCP checksum field");
 
+  // whole datagrams as the link endpoint writes them (ipv4.WritePacket after
+  // sendTCP): with both checksum fields zeroed, TX_DATAGRAM in place restores the
+  // harness's bytes exactly, and its two results per datagram are those fields
+  std::vector<uint8_t> dblank(blob);
+  for (uint64_t i = 0; i < n; ++i) {
+    dblank[off[i] + 10] = dblank[off[i] + 11] = 0;
+    dblank[off[i] + 20 + 16] = dblank[off[i] + 20 + 17] = 0;
+  }
+  std::vector<uint16_t> two(2 * n, 0xAAAA);
+  batch::HostRagged(dblank.data(), off.data(), n, batch::TX_DATAGRAM, two.data());
+  for (uint64_t i = 0; i < n; ++i) {
+    EXPECT(two[2 * i] == header::IPv4{blob.data() + off[i]}.Checksum(), "dg ipv4 field %lu", i);
+    EXPECT(two[2 * i + 1] == fields[i], "dg tcp field %lu", i);
+  }
+  uint8_t *d_dg;
+  HIPCK(hipMalloc(&d_dg, dblank.size()));
+  HIPCK(hipMemcpy(d_dg, dblank.data(), dblank.size(), hipMemcpyHostToDevice));
+  batch::FillRagged(d_dg, d_off, n, batch::TX_DATAGRAM, nullptr);
+  std::vector<uint8_t> filled(dblank.size());
+  HIPCK(hipMemcpy(filled.data(), d_dg, filled.size(), hipMemcpyDeviceToHost));
+  EXPECT(filled == blob, "device TX_DATAGRAM fill restores both fields of every datagram");
+  HIPCK(hipFree(d_dg));
+  batch::FillHostRagged(dblank.data(), off.data(), n, batch::TX_DATAGRAM, nullptr);
+  EXPECT(dblank == blob, "host TX_DATAGRAM fill restores both fields of every datagram");
+
   bool threw = false;
   try {
     batch::Uniform(d_segs, 16, 70000, 1, batch::TCP, d_out);
