@@ -64,7 +64,7 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e1));
   uint16_t *out, *init;
   uint8_t *addrs;
-  CK(hipMalloc(&out, n * 2));
+  CK(hipMalloc(&out, n * 4));  // up to 2 results per packet (YU_MODE_OUTPUTS)
   CK(hipMalloc(&init, n * 2));
   CK(hipMalloc(&addrs, n * 8));
   fill<<<1024, 256>>>((uint8_t *)init, n * 2, 11);
