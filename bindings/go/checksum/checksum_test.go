@@ -151,3 +151,47 @@ func TestShortArgumentsRejected(t *testing.T) {
 		t.Fatal("fill: short initial accepted")
 	}
 }
+
+// TestFillTxDatagram: ModeTxDatagram sets both fields of whole outgoing IPv4
+// datagrams (header checksum at 10, UDP checksum at 20+6); out receives the two
+// values per datagram. Afterwards the header sums to 0xFFFF and so does the UDP
+// segment with its pseudo-header (checked with the scalar package, as
+// network/ipv4/ipv4.go and transport/udp do on receive).
+func TestFillTxDatagram(t *testing.T) {
+	pkts := make([][]byte, 300)
+	for i := range pkts {
+		n := 28 + (i*41)%1400
+		p := make([]byte, n)
+		for j := range p {
+			p[j] = byte(i*7 + j*13)
+		}
+		p[0], p[9] = 0x45, 17 // IPv4, IHL 5, UDP
+		p[2], p[3] = byte(n>>8), byte(n)
+		p[24], p[25] = byte((n-20)>>8), byte(n-20)
+		pkts[i] = p
+	}
+	out := make([]uint16, 2*len(pkts))
+	if FillHostPackets(pkts, ModeTxDatagram, nil, nil, out[:len(pkts)], 0) == nil {
+		t.Fatal("out with one slot per datagram accepted")
+	}
+	if err := FillHostPackets(pkts, ModeTxDatagram, nil, nil, out, 0); err == ErrNoDevice {
+		t.Skip("no HIP device")
+	} else if err != nil {
+		t.Fatal(err)
+	}
+	for i, p := range pkts {
+		if s := Checksum(p[:20], 0); s != 0xffff {
+			t.Fatalf("datagram %d: header sums to %#x", i, s)
+		}
+		if got := uint16(p[10])<<8 | uint16(p[11]); got != out[2*i] {
+			t.Fatalf("datagram %d: header field %#x, out %#x", i, got, out[2*i])
+		}
+		ph := Checksum(p[12:20], 17+uint16(len(p)-20))
+		if s := Checksum(p[20:], ph); s != 0xffff {
+			t.Fatalf("datagram %d: UDP segment sums to %#x", i, s)
+		}
+		if got := uint16(p[26])<<8 | uint16(p[27]); got != out[2*i+1] {
+			t.Fatalf("datagram %d: UDP field %#x, out %#x", i, got, out[2*i+1])
+		}
+	}
+}
