@@ -42,6 +42,21 @@ __global__ void set_ihl_stride(uint8_t *p, uint64_t stride, uint64_t n) {
   for (; i < n; i += (uint64_t)gridDim.x * blockDim.x) p[i * stride] = 0x45;
 }
 
+// Well-formed TCP/IPv4 datagrams (kbench config 15): IHL 5, TotalLength = the
+// packet length, protocol 6, DataOffset 5, as bench config 11 builds them
+__global__ void set_dg(uint8_t *p, const uint64_t *off, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint8_t *b = p + off[i];
+    const uint64_t len = off[i + 1] - off[i];
+    b[0] = 0x45;
+    b[2] = (uint8_t)(len >> 8);
+    b[3] = (uint8_t)len;
+    b[9] = 6;
+    if (len > 32) b[32] = 0x50;
+  }
+}
+
 static void on_segv(int sig) {
   void *bt[64];
   const int k = backtrace(bt, 64);
@@ -85,16 +100,19 @@ int main(int argc, char **argv) {
       bytes = n * L;
       alg = bytes + 10 * n;
     }
-    if (cfg >= 4 && cfg <= 12) {
+    if ((cfg >= 4 && cfg <= 12) || cfg == 15) {
       // 4: BASELINE config 4 (U{64..9000}); 5: tun-like U{64..1500}; 6: U{40..200}
       // (RAW + initial); 7: U{64..1500} TCP segments, 8: U{40..200} UDP (TX kinds, addrs)
       // 9: U{40..600}, 10: U{40..1000} (RAW + initial): small-grid crossover
       const int lo = (cfg == 4 || cfg == 5 || cfg == 7) ? 64 : 40;
-      const int hi = cfg == 4 ? 9000 : ((cfg == 5 || cfg == 7 || cfg == 11 || cfg == 12) ? 1500 : (cfg == 9 ? 600 : (cfg == 10 ? 1000 : 200)));
+      const int hi = cfg == 4 ? 9000 : ((cfg == 5 || cfg == 7 || cfg == 11 || cfg == 12 || cfg == 15) ? 1500 : (cfg == 9 ? 600 : (cfg == 10 ? 1000 : 200)));
       // 11: U{40..1500} IPv4 datagrams, header checksum only (k_rag)
       if (cfg == 11 || cfg == 12) mode = YU_MODE_IPV4;  // 12: IHL 5 in every header
       if (cfg == 7) mode = YU_MODE_TCP;
       if (cfg == 8) mode = YU_MODE_UDP;
+      // 15: U{40..1500} well-formed TCP/IPv4 datagrams, both TX fields (bench
+      // config 11; KB_MODE=8 verifies the same bytes)
+      if (cfg == 15) mode = YU_MODE_TX_DATAGRAM;
       std::mt19937_64 rng(4);
       std::uniform_int_distribution<int> d(lo, hi);
       std::vector<uint64_t> off(n + 1, 0);
@@ -103,6 +121,7 @@ int main(int argc, char **argv) {
       for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + (a4 ? (d(rng) + 3) & ~3 : d(rng));
       bytes = off[n];
       alg = bytes + 8 * (n + 1) + (mode == YU_MODE_RAW ? 4 : 10) * n;
+      if (cfg == 15) alg = bytes + 8 * (n + 1) + 4 * n;  // two results per datagram
       if (mode == YU_MODE_IPV4) alg = 40 * n + 8 * (n + 1) + 2 * n;  // ~mean IHL*4 of random headers
       CK(hipMalloc(&d_off, (n + 1) * 8));
       CK(hipMemcpy(d_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
@@ -116,6 +135,7 @@ int main(int argc, char **argv) {
       CK(hipMalloc(&bufs[r], bytes + 64));
       fill<<<4096, 256>>>(bufs[r], bytes + 64, 100 + r);
       if (cfg == 12) set_ihl<<<1024, 256>>>(bufs[r], d_off, n);
+      if (cfg == 15) set_dg<<<1024, 256>>>(bufs[r], d_off, n);
       if (cfg == 13) set_ihl_stride<<<1024, 256>>>(bufs[r], L, n);
     }
     CK(hipDeviceSynchronize());

@@ -1490,22 +1490,25 @@ struct SegRx {
   uint32_t proto;
   uint32_t ipf;     // TX_DATAGRAM: LE sum of the IPv4 checksum field's bytes
   uint32_t hl;      // TX_DATAGRAM: header length (0 outside the contract)
+  uint32_t fo;      // TX_DATAGRAM: transport field offset in the packet (0: none)
 };
 
 // TX_DATAGRAM on a parsed header (rx_parse): the datagram is in contract when
 // 20 <= HeaderLength() <= TotalLength() <= len; its transport field exists
 // when the protocol is UDP / TCP / ICMP and the segment holds its header.
-// Returns the transport field offset from the packet start (0: none) and
-// records the IPv4 field's bytes (window bytes sh+10, sh+11) for subtraction.
+// Returns (and records in rx.fo) the transport field offset from the packet
+// start (0: none), and records the IPv4 field's bytes 10 and 11 as the
+// address-ordered LE sum they add to (byte 10 is a low byte when the packet
+// starts at an even address) for subtraction.
 __device__ __forceinline__ uint32_t dg_parse(SegRx &rx, uint32_t sh, uint32_t hl, uint32_t tl) {
   const bool ok = !(rx.flags & YU_RX_INVALID) && hl >= 20u;
   rx.hl = ok ? hl : 0u;
-  uint32_t f = 0;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) f = sad(rx.h[j] & byte_range_mask(4u * (uint32_t)j, sh + 10u, sh + 12u), f);
-  rx.ipf = f;
+  const uint32_t w2 = sh ? __builtin_amdgcn_alignbyte(rx.h[3], rx.h[2], sh) : rx.h[2];  // bytes 8..11
+  const uint32_t f = w2 >> 16;
+  rx.ipf = (sh & 1u) ? ((f >> 8) | ((f & 0xFFu) << 8)) : f;
   const uint32_t fo = l4_field(rx.proto);
-  return ok && fo && tl - hl >= l4_min(rx.proto) ? hl + fo : 0u;
+  rx.fo = ok && fo && tl - hl >= l4_min(rx.proto) ? hl + fo : 0u;
+  return rx.fo;
 }
 
 // A 16-bit field value stored big-endian (binary.BigEndian.PutUint16).
@@ -1570,17 +1573,17 @@ __device__ __forceinline__ uint64_t seg_waves(const BatchArgs &A) {
 // carries no code or registers for the others): plain (RAW / VERIFY_TCP /
 // VERIFY_UDP: start and end), TX (UDP / TCP / ICMP: + the checksum field's
 // two ends), RX (VERIFY_RX: + header and transport ends), DG (TX_DATAGRAM:
-// RX's points + the transport field's two ends; the IPv4 field comes off the
-// parsed header's registers).
+// RX's points; the IPv4 field comes off the parsed header's registers and
+// the transport field's two bytes are read from the tile that holds them).
 constexpr int kSegPlain = 0, kSegTx = 1, kSegRx = 2, kSegDg = 3;
 
-// (the DG kind asks for at least 3 waves per SIMD: its two extra points would
-// otherwise take it to 170 VGPRs, 2 waves; the other kinds are left alone)
+// (the DG kind asks for at least 3 waves per SIMD, which it would otherwise
+// miss by a few VGPRs; the other kinds are left alone)
 template <int U, int NT, int K, int CH = 64>
 __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   constexpr bool DG = K == kSegDg;
   constexpr bool RX = K == kSegRx || DG;  // parses each packet's IPv4 header
-  constexpr int NP = K == kSegPlain ? 2 : (DG ? 6 : 4);  // point slots in use
+  constexpr int NP = K == kSegPlain ? 2 : 4;  // point slots in use
   constexpr uint32_t T = 64u * 16u * U;
   constexpr uint32_t NC = 64u * U;  // chunks per tile
   __shared__ uint4 s_data[4][NC];   // the tile's bytes
@@ -1607,9 +1610,14 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   seg_geom(data, A.n, ch * CH, cur);
 
   // per-chunk state
-  SegPt pt[6];  // start, end, then field start/end (TX) or header/transport end (RX),
-                // then (DG) the transport field's start/end; slots past NP unused
+  SegPt pt[4];  // start, end, then field start/end (TX) or header/transport end (RX)
   SegRx rx;
+  // DG: the transport field's next unread byte (kNoPt: none or done), the bytes
+  // of it still to read (2, or 1 when the field straddles two tiles) and the
+  // address-ordered LE sum of those read (P(field end) - P(field start) without
+  // two more point evaluations per tile)
+  uint64_t fx = 0;
+  uint32_t fk = 0, fsum = 0;
   bool exact = false;
   uint32_t carry_l = 0, carry_t = 0;
   auto begin_chunk = [&](const SegChunk &k) __attribute__((always_inline)) {
@@ -1628,10 +1636,13 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
       rx.need = len >= 20u ? (1u << (((19u + sh) >> 2) + 1u)) - 1u : 0u;
       rx.flags = YU_RX_INVALID;
       rx.pseudo = rx.proto = 0u;
-      rx.ipf = rx.hl = 0u;
+      rx.ipf = rx.hl = rx.fo = 0u;
 #pragma unroll
       for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
-      if (DG) pt[2].x = pt[3].x = pt[4].x = pt[5].x = kNoPt;
+      if (DG) {
+        pt[2].x = pt[3].x = fx = kNoPt;
+        fk = fsum = 0u;
+      }
     }
 #pragma unroll
     for (int i = 0; i < NP; ++i) pt[i].p = pt[i].t = 0u;
@@ -1681,6 +1692,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
     bool here = false;
 #pragma unroll
     for (int i = 0; i < NP; ++i) here |= pt[i].x - tb < T;
+    if (DG) here |= fx - tb < T;
     if (RX) {  // a header window [floor4(start), +24) still being gathered
       const uint64_t hs = pt[0].x & ~3ull;
       here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
@@ -1714,8 +1726,8 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
               pt[3].x = pt[0].x + tl;
             }
             if (fo) {
-              pt[4].x = pt[0].x + fo;
-              pt[5].x = pt[0].x + fo + 2u;
+              fx = pt[0].x + fo;
+              fk = 2u;
             }
           } else {
             pt[2].x = pt[0].x + hl;
@@ -1730,6 +1742,21 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
         if (q < T) {
           const uint32_t k = (uint32_t)q >> 4;
           pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
+        }
+      }
+      if (DG) {  // the transport field's bytes, weighted by address parity
+        const uint64_t q = fx - tb;
+        if (q < T) {
+          const uint8_t *sb = (const uint8_t *)s_data[wid];
+          const uint32_t b = sb[q];
+          fsum += (q & 1u) ? b << 8 : b;
+          if (fk == 2u && q + 1u < T) {
+            const uint32_t b1 = sb[q + 1u];
+            fsum += (q & 1u) ? b1 : b1 << 8;
+          }
+          const bool split = fk == 2u && q + 1u == T;  // the field's second byte opens the next tile
+          fk = split ? 1u : 0u;
+          fx = split ? fx + 1u : kNoPt;
         }
       }
       if (RX && !DG && parsed) {
@@ -1798,16 +1825,18 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
         // sendICMPv4, see include/yucsum.h)
         uint32_t ip = 0u, l4 = 0u;
         if (rx.hl) ip = ~fold32(le_to_be(pt[2].p - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
-        const bool has_l4 = pt[4].x != kNoPt;
-        if (has_l4)
-          l4 = ~fold32(le_to_be(pt[3].p - pt[2].p - (pt[5].p - pt[4].p), odd) + rx.pseudo) & 0xFFFFu;
-        if (A.out) {
-          A.out[2u * p] = (uint16_t)ip;
-          A.out[2u * p + 1u] = (uint16_t)l4;
+        if (rx.fo) l4 = ~fold32(le_to_be(pt[3].p - pt[2].p - fsum, odd) + rx.pseudo) & 0xFFFFu;
+        if (A.out) {  // out[2p], out[2p + 1]: one 32-bit store when aligned
+          if (((uintptr_t)A.out & 3u) == 0u) {
+            ((uint32_t *)A.out)[p] = ip | (l4 << 16);
+          } else {
+            A.out[2u * p] = (uint16_t)ip;
+            A.out[2u * p + 1u] = (uint16_t)l4;
+          }
         }
         if (A.fill) {
           if (rx.hl) put_be16(A.fill + cur.ox + 10u, ip);
-          if (has_l4) put_be16(A.fill + cur.ox + (pt[4].x - pt[0].x), l4);
+          if (rx.fo) put_be16(A.fill + cur.ox + rx.fo, l4);
         }
       } else if (RX) {
         // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
