@@ -1583,7 +1583,9 @@ template <int U, int NT, int K, int CH = 64>
 __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   constexpr bool DG = K == kSegDg;
   constexpr bool RX = K == kSegRx || DG;  // parses each packet's IPv4 header
-  constexpr int NP = K == kSegPlain ? 2 : 4;  // point slots in use
+  constexpr bool tx = K == kSegTx;
+  constexpr bool FB = tx || DG;                 // a field whose bytes are read from the tile
+  constexpr int NP = K == kSegRx || DG ? 4 : 2;  // point slots in use
   constexpr uint32_t T = 64u * 16u * U;
   constexpr uint32_t NC = 64u * U;  // chunks per tile
   __shared__ uint4 s_data[4][NC];   // the tile's bytes
@@ -1593,7 +1595,6 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   const uint64_t wave = grid_wave(A.xcd);
   const uint64_t nwave = seg_waves(A);
   const int mode = A.mode;
-  constexpr bool tx = K == kSegTx;
   const uint32_t fld = mode_field(mode);
   const SidePtrs sp = side_ptrs(A);
   const uint64_t data = (uint64_t)(uintptr_t)A.data;
@@ -1610,12 +1611,12 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   seg_geom(data, A.n, ch * CH, cur);
 
   // per-chunk state
-  SegPt pt[4];  // start, end, then field start/end (TX) or header/transport end (RX)
+  SegPt pt[4];  // start, end, then (RX, DG) header and transport end
   SegRx rx;
-  // DG: the transport field's next unread byte (kNoPt: none or done), the bytes
-  // of it still to read (2, or 1 when the field straddles two tiles) and the
-  // address-ordered LE sum of those read (P(field end) - P(field start) without
-  // two more point evaluations per tile)
+  // TX, DG: the checksum field's next unread byte (kNoPt: none or done; DG: the
+  // transport field), the bytes of it still to read (2, or 1 when the field
+  // straddles two tiles) and the address-ordered LE sum of those read:
+  // P(field end) - P(field start) without two more point evaluations per tile
   uint64_t fx = 0;
   uint32_t fk = 0, fsum = 0;
   bool exact = false;
@@ -1628,9 +1629,12 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
     // ragged packets lie back to back: P(end) is the next lane's P(start), so
     // only lane 63 evaluates an end point (the chunk end); RX needs none
     pt[1].x = RX || (contig && lane != 63u) ? kNoPt : y;
-    const bool f = tx && fld + 2u <= len;  // TX: the checksum field's ends
-    pt[2].x = f ? x + fld : kNoPt;
-    pt[3].x = f ? x + fld + 2u : kNoPt;
+    if (tx) {  // the checksum field, when the packet holds it
+      const bool f = fld + 2u <= len;
+      fx = f ? x + fld : kNoPt;
+      fk = f ? 2u : 0u;
+      fsum = 0u;
+    }
     if (RX) {  // header and transport ends, once the header is parsed
       const uint32_t sh = (uint32_t)x & 3u;
       rx.need = len >= 20u ? (1u << (((19u + sh) >> 2) + 1u)) - 1u : 0u;
@@ -1692,7 +1696,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
     bool here = false;
 #pragma unroll
     for (int i = 0; i < NP; ++i) here |= pt[i].x - tb < T;
-    if (DG) here |= fx - tb < T;
+    if (FB) here |= fx - tb < T;
     if (RX) {  // a header window [floor4(start), +24) still being gathered
       const uint64_t hs = pt[0].x & ~3ull;
       here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
@@ -1744,7 +1748,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
           pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
         }
       }
-      if (DG) {  // the transport field's bytes, weighted by address parity
+      if (FB) {  // the field's bytes, weighted by address parity
         const uint64_t q = fx - tb;
         if (q < T) {
           const uint8_t *sb = (const uint8_t *)s_data[wid];
@@ -1860,7 +1864,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
           const uint32_t a = S - b;              // even-address bytes
           v = odd ? a + (b << 8) : (a << 8) + b;
         } else {
-          v = le_to_be(pe - pt[0].p - (tx ? pt[3].p - pt[2].p : 0u), odd);
+          v = le_to_be(pe - pt[0].p - (tx ? fsum : 0u), odd);
         }
         const uint64_t len = cur.oy - cur.ox;
         finish_packet(A, p, v, len, cur.sd, A.fill ? A.fill + cur.ox : nullptr,
