@@ -127,6 +127,10 @@ def test_argument_validation_precedes_device():
                                     o, 0) == _lib.YU_EINVAL
     assert L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 1, 10, None, 0, None,
                                     o, 0) == _lib.YU_EINVAL  # mode
+    # view lengths whose sum wraps 64 bits to a small packet are refused, not summed
+    huge = (_lib.YuIovec * 2)(_lib.YuIovec(p, 1 << 63), _lib.YuIovec(p, (1 << 63) + 4))
+    assert L.yu_csum_batch_host_iov(ctypes.addressof(huge), ctypes.addressof(first), 1, 0, None, 0, None,
+                                    o, 0) == _lib.YU_EINVAL
     # multi-GPU host calls: device list and batch checked before any device work
     devs = (ctypes.c_int * 2)(0, 0)
     pd = ctypes.addressof(devs)

@@ -32,6 +32,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -586,9 +587,9 @@ int check_iov(const yu_iovec *iov, const uint64_t *first_iov, uint64_t n, int mo
     uint64_t l = 0;
     for (uint64_t v = first_iov[i]; v < first_iov[i + 1]; ++v) {
       if (!iov[v].base && iov[v].len) return YU_EINVAL;
+      if (iov[v].len > cap - l) return YU_EINVAL;  // l <= cap: no wrap, even for huge views
       l += iov[v].len;
     }
-    if (l > cap) return YU_EINVAL;
   }
   return YU_OK;
 }
@@ -890,14 +891,16 @@ void set_fields(uint64_t n, int mode, const uint16_t *res, const At &at) {
   for (uint64_t i = 0; i < n; ++i) one(i);
 }
 
-// Results into the caller's array, or a scratch one when it passes none.
+// Results into the caller's array, or a scratch one when it passes none
+// (p stays null when that allocation fails: the call returns YU_ENOMEM, no
+// exception crosses the C ABI).
 struct ResultBuf {
-  std::vector<uint16_t> tmp;
+  std::unique_ptr<uint16_t[]> tmp;
   uint16_t *p;
   ResultBuf(uint16_t *out, uint64_t n) : p(out) {  // n = results, not packets
     if (!p) {
-      tmp.resize(n ? n : 1);
-      p = tmp.data();
+      tmp.reset(new (std::nothrow) uint16_t[n ? n : 1]);
+      p = tmp.get();
     }
   }
 };
@@ -911,6 +914,7 @@ extern "C" int yu_csum_fill_host_uniform(uint8_t *h_data, uint64_t stride, uint3
   if (!tx_mode(mode)) return YU_EINVAL;
   if (n == 0) return YU_OK;
   ResultBuf r(h_out, n * YU_MODE_OUTPUTS(mode));
+  if (!r.p) return YU_ENOMEM;
   int rc = yu_csum_batch_host_uniform(h_data, stride, len, n, mode, h_initial_arr, initial,
                                       h_addrs, r.p, device);
   if (rc) return rc;
@@ -927,6 +931,7 @@ extern "C" int yu_csum_fill_host_ragged(uint8_t *h_data, const uint64_t *h_offse
   if (!tx_mode(mode)) return YU_EINVAL;
   if (n == 0) return YU_OK;
   ResultBuf r(h_out, n * YU_MODE_OUTPUTS(mode));
+  if (!r.p) return YU_ENOMEM;
   int rc = yu_csum_batch_host_ragged(h_data, h_offsets, n, mode, h_initial_arr, initial, h_addrs,
                                      r.p, device);
   if (rc) return rc;
@@ -942,6 +947,7 @@ extern "C" int yu_csum_fill_host_iov(const yu_iovec *iov, const uint64_t *first_
   if (!tx_mode(mode)) return YU_EINVAL;
   if (n == 0) return YU_OK;
   ResultBuf r(h_out, n * YU_MODE_OUTPUTS(mode));
+  if (!r.p) return YU_ENOMEM;
   int rc = yu_csum_batch_host_iov(iov, first_iov, n, mode, h_initial_arr, initial, h_addrs, r.p,
                                   device);
   if (rc) return rc;
