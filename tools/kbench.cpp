@@ -100,7 +100,7 @@ int main(int argc, char **argv) {
       bytes = n * L;
       alg = bytes + 10 * n;
     }
-    if ((cfg >= 4 && cfg <= 12) || cfg == 15) {
+    if ((cfg >= 4 && cfg <= 12) || cfg == 15 || cfg == 16) {
       // 4: BASELINE config 4 (U{64..9000}); 5: tun-like U{64..1500}; 6: U{40..200}
       // (RAW + initial); 7: U{64..1500} TCP segments, 8: U{40..200} UDP (TX kinds, addrs)
       // 9: U{40..600}, 10: U{40..1000} (RAW + initial): small-grid crossover
@@ -113,6 +113,8 @@ int main(int argc, char **argv) {
       // 15: U{40..1500} well-formed TCP/IPv4 datagrams, both TX fields (bench
       // config 11; KB_MODE=8 verifies the same bytes)
       if (cfg == 15) mode = YU_MODE_TX_DATAGRAM;
+      // 16: U{40..200} well-formed datagrams, VERIFY_RX (bench config 7)
+      if (cfg == 16) mode = YU_MODE_VERIFY_RX;
       std::mt19937_64 rng(4);
       std::uniform_int_distribution<int> d(lo, hi);
       std::vector<uint64_t> off(n + 1, 0);
@@ -122,6 +124,7 @@ int main(int argc, char **argv) {
       bytes = off[n];
       alg = bytes + 8 * (n + 1) + (mode == YU_MODE_RAW ? 4 : 10) * n;
       if (cfg == 15) alg = bytes + 8 * (n + 1) + 4 * n;  // two results per datagram
+      if (cfg == 16) alg = bytes + 8 * (n + 1) + 2 * n;
       if (mode == YU_MODE_IPV4) alg = 40 * n + 8 * (n + 1) + 2 * n;  // ~mean IHL*4 of random headers
       CK(hipMalloc(&d_off, (n + 1) * 8));
       CK(hipMemcpy(d_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
@@ -135,7 +138,7 @@ int main(int argc, char **argv) {
       CK(hipMalloc(&bufs[r], bytes + 64));
       fill<<<4096, 256>>>(bufs[r], bytes + 64, 100 + r);
       if (cfg == 12) set_ihl<<<1024, 256>>>(bufs[r], d_off, n);
-      if (cfg == 15) set_dg<<<1024, 256>>>(bufs[r], d_off, n);
+      if (cfg == 15 || cfg == 16) set_dg<<<1024, 256>>>(bufs[r], d_off, n);
       if (cfg == 13) set_ihl_stride<<<1024, 256>>>(bufs[r], L, n);
     }
     CK(hipDeviceSynchronize());

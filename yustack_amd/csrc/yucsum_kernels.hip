@@ -1491,6 +1491,8 @@ struct SegRx {
   uint32_t ipf;     // TX_DATAGRAM: LE sum of the IPv4 checksum field's bytes
   uint32_t hl;      // TX_DATAGRAM: header length (0 outside the contract)
   uint32_t fo;      // TX_DATAGRAM: transport field offset in the packet (0: none)
+  uint32_t h20;     // k_seg: the header is the plain 20 bytes (IHL 5) of a valid packet
+  uint32_t hsum;    // k_seg: then the address-ordered LE sum of those 20 bytes
 };
 
 // TX_DATAGRAM on a parsed header (rx_parse): the datagram is in contract when
@@ -1534,6 +1536,14 @@ __device__ __forceinline__ void rx_parse(SegRx &rx, uint32_t sh, uint64_t len, u
   tl = ((w[0] >> 8) & 0xFF00u) | (w[0] >> 24);            // TotalLength(), BE
   const uint32_t proto = (w[2] >> 8) & 0xFFu;             // Protocol()
   const bool valid = hl <= tl && tl <= len;               // IsValid (len >= 20 checked)
+  // The usual 20-byte header is wholly in registers: its sum in the order of
+  // the stream's LE prefix sums (byte 0 is a low byte when the packet starts
+  // at an even address), so k_seg needs no point at the header end.
+  uint32_t hs = 0;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) hs = (sh & 1u) ? sadperm(w[j], kSelSwap, hs) : sad(w[j], hs);
+  rx.hsum = hs;
+  rx.h20 = valid && hl == 20u;
   const bool l4 = valid && (proto == 6u || proto == 17u || proto == 1u);
   rx.flags = valid ? 0u : YU_RX_INVALID;
   if (l4) rx.flags |= YU_RX_L4;
@@ -1640,7 +1650,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
       rx.need = len >= 20u ? (1u << (((19u + sh) >> 2) + 1u)) - 1u : 0u;
       rx.flags = YU_RX_INVALID;
       rx.pseudo = rx.proto = 0u;
-      rx.ipf = rx.hl = rx.fo = 0u;
+      rx.ipf = rx.hl = rx.fo = rx.h20 = rx.hsum = 0u;
 #pragma unroll
       for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
       if (DG) {
@@ -1726,7 +1736,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
             // byte 20, so never in a tile that has gone by
             const uint32_t fo = dg_parse(rx, (uint32_t)pt[0].x & 3u, hl, tl);
             if (rx.hl) {
-              pt[2].x = pt[0].x + hl;
+              pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
               pt[3].x = pt[0].x + tl;
             }
             if (fo) {
@@ -1734,7 +1744,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
               fk = 2u;
             }
           } else {
-            pt[2].x = pt[0].x + hl;
+            pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
             pt[3].x = pt[0].x + tl;
           }
           parsed = true;
@@ -1828,8 +1838,9 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
         // pseudo header + length from the datagram (sendUDP / sendTCP /
         // sendICMPv4, see include/yucsum.h)
         uint32_t ip = 0u, l4 = 0u;
-        if (rx.hl) ip = ~fold32(le_to_be(pt[2].p - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
-        if (rx.fo) l4 = ~fold32(le_to_be(pt[3].p - pt[2].p - fsum, odd) + rx.pseudo) & 0xFFFFu;
+        const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
+        if (rx.hl) ip = ~fold32(le_to_be(p2 - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
+        if (rx.fo) l4 = ~fold32(le_to_be(pt[3].p - p2 - fsum, odd) + rx.pseudo) & 0xFFFFu;
         if (A.out) {  // out[2p], out[2p + 1]: one 32-bit store when aligned
           if (((uintptr_t)A.out & 3u) == 0u) {
             ((uint32_t *)A.out)[p] = ip | (l4 << 16);
@@ -1847,10 +1858,11 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
         // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
         uint32_t r = rx.flags;
         if (!(r & YU_RX_INVALID)) {
-          const uint32_t ip = fold32(le_to_be(pt[2].p - pt[0].p, odd));
+          const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
+          const uint32_t ip = fold32(le_to_be(p2 - pt[0].p, odd));
           if (ip == 0u || ip == 0xFFFFu) r |= YU_RX_IP_OK;
           if (r & YU_RX_L4) {
-            const uint32_t l4 = fold32(le_to_be(pt[3].p - pt[2].p, odd) + rx.pseudo);
+            const uint32_t l4 = fold32(le_to_be(pt[3].p - p2, odd) + rx.pseudo);
             if (l4 == 0u || l4 == 0xFFFFu) r |= YU_RX_L4_OK;
           }
         }
