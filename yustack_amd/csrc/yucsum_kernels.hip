@@ -2242,9 +2242,16 @@ int env_int(const char *name, int lo, int hi, int dflt) {
 // about 4 steps with the next in flight): 1M x 64 B 14.2 -> 13.4 us, 72 B 16.0
 // -> 14.8, 32 B 10.4 -> 8.4, 100 B 21.7 -> 20.8, 124 B 25.0 -> 23.8
 // (profiles/r02/kbench_ab_lane_grid.log).
-int blocks_per_cu(uint32_t G, bool step64) {
+// Uniform batches on 4 KiB k_seg tiles (dense 129..447-byte packets, `seg4u`)
+// run on 10: each wave then streams 2-3 chunks with the next tile in flight
+// instead of one chunk per wave (1M UDP datagrams, medians of 6 launches of
+// 30: 136 B 33.0 -> 30.5 us, 160 B 34.5 -> 32.9, 256 B 50.2 -> 47.8, 320 B
+// 58.8 -> 56.9, 384 B 70.3 -> 66.7, 200 and 420 B within 1 %;
+// profiles/r02/kbench_grid_mid_uniform_{a,b}.log).
+int blocks_per_cu(uint32_t G, bool step64, bool seg4u) {
   static int v = env_int("YU_BLOCKS_PER_CU", 1, 1024, 0);
   if (v) return v;
+  if (seg4u) return 10;
   return step64 ? 6 : (G < 16 ? 16 : 64);
 }
 
@@ -2281,7 +2288,8 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_status(e);
   const uint64_t waves_per_block = 4;
-  const uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu(v.G, is_tiny(v));
+  const bool seg4u = !A.offsets && (&v == &kSeg4 || &v == &kSegTx4);
+  const uint64_t cap = (uint64_t)cu_count(dev) * (uint64_t)blocks_per_cu(v.G, is_tiny(v), seg4u);
   // k_small: runs from 8 runs per CU up (1500-B packets, runs vs interleaved:
   // 16384 packets 8.0 vs 7.2 us, 32768 11.3 vs 12.5, 131072 35.3 vs 38.8; 768-B
   // packets 6.6 vs 5.0, 7.5 vs 8.2, 19.7 vs 22.0; kbench_ab_k_small_runs.log)
