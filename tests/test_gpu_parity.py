@@ -968,6 +968,34 @@ def test_k_small_runs_at_grid_size(dev, oracle_c, stride, length, mode, align, n
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
 
 
+@pytest.mark.parametrize("mode", ["tcp", "udp"])
+@pytest.mark.parametrize("length,gap,n", [
+    (1280, 0, 40000 + 3), (1281, 3, 40000 + 5), (1283, 1, 33000 + 1), (1390, 2, 40000 + 15),
+    (1500, 0, 40000 + 9), (1500, 100, 65536 + 1), (1534, 2, 40000 + 7), (1535, 1, 32768 + 11),
+])
+def test_k_small_mtu_send_path(dev, oracle_c, mode, length, gap, n):
+    """The MTU send path (config 3's shape: TCP or UDP with {src,dst} records, no
+    initial array, 4-aligned packet starts, 1280..1535-byte packets on k_small<16,6>
+    runs), at its edges: every length residue mod 4 (the last dword's tail mask),
+    both ends of the length range where only the window's last step is partial,
+    gaps between packets, partial last runs; bit-exact against the oracle."""
+    mod = {"udp": O.MODE_UDP, "tcp": O.MODE_TCP}[mode]
+    stride = (length + 3) // 4 * 4 + 4 * gap
+    assert batch.variant(stride, length, mode, 0, n=n) == "k_small<16,6>"
+    assert n // 16 >= 8 * torch.cuda.get_device_properties(dev).multi_processor_count  # runs
+    g = torch.Generator(device=dev)
+    g.manual_seed(length * 7 + gap)
+    total = (n - 1) * stride + length
+    d = torch.randint(0, 256, (total + 16,), dtype=torch.uint8, device=dev, generator=g)
+    if mode == "tcp":  # DataOffset 5
+        d[12: 12 + (n - 1) * stride + 1: stride] = 0x50
+    ad = torch.randint(0, 256, (8 * n,), dtype=torch.uint8, device=dev, generator=g)
+    got = batch.checksum_uniform(d, stride, length, n, mode, addrs=ad).cpu().numpy()
+    want = oracle_c.batch(d.cpu().numpy(), mod, stride=stride, length=length, n=n,
+                          addrs=ad.cpu().numpy(), threads=8)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
 def test_full_size_fill_then_verify_round_trip(dev):
     """Size-independent property at BASELINE config 3 and 4 sizes: writing the TX
     field in place (yu_csum_fill_*, SetChecksum semantics) and then verifying the same
