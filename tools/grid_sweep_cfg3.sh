@@ -1,0 +1,19 @@
+# Config 3 (k_small<16,6> runs) grid sweep (measurement only).
+set -o pipefail
+mkdir -p gpurun_out
+args=()
+for rep in 1 2 3; do
+  for b in 0 5 8 10 16 20 32 48; do
+    if [ "$b" = 0 ]; then args+=("3"); else args+=("3 YU_BLOCKS_PER_CU=$b"); fi
+  done
+done
+bash tools/ab.sh "${args[@]}" > gpurun_out/grid_cfg3.log 2>&1 || { tail gpurun_out/grid_cfg3.log; exit 1; }
+python3 - <<'PY'
+import re,collections
+cur=None; d=collections.defaultdict(list)
+for l in open('gpurun_out/grid_cfg3.log'):
+    if l.startswith('=='): cur=l.strip()[3:]
+    m=re.search(r'round (\d):\s+([\d.]+) us',l)
+    if m and cur and m.group(1) != '0': d[cur].append(float(m.group(2)))
+for k,v in sorted(d.items()): print(f"{k:40s} min {min(v):6.1f} med {sorted(v)[len(v)//2]:6.1f}")
+PY
