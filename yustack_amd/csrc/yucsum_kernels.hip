@@ -116,10 +116,6 @@ __host__ __device__ __forceinline__ bool mode_is_tx(int m) {
 __host__ __device__ __forceinline__ bool mode_fills(int m) {
   return mode_is_tx(m) || m == YU_MODE_TX_DATAGRAM;
 }
-// Results per packet in out (include/yucsum.h YU_MODE_OUTPUTS).
-__host__ __device__ __forceinline__ uint32_t mode_outputs(int m) {
-  return m == YU_MODE_TX_DATAGRAM ? 2u : 1u;
-}
 // Offset of the transport checksum field in a segment of IPv4 protocol
 // `proto`, and the segment's minimum length (UDP 6/8, TCP 16/20, ICMP 2/4);
 // 0 / 0 for other protocols.
