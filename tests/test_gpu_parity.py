@@ -19,7 +19,10 @@ EDGE_LENS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 20, 31, 32, 33, 60, 63, 64, 65,
 
 
 def _to(dev, a):
-    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    a = np.ascontiguousarray(a)
+    if not a.flags.writeable:  # e.g. golden vectors from np.frombuffer
+        a = a.copy()
+    return torch.from_numpy(a).to(dev)
 
 
 def _rand(rng, n, kind="rand"):
