@@ -7,6 +7,12 @@ configuration the north-star target (>=70 % of HBM peak) is quoted on; with
 --gpus N every rank processes its own 1M-segment shard (config 5 = 8 x config 3,
 weak scaling, no data-path collective — packets are independent).
 
+Launch: under torch.distributed.run (WORLD_SIZE set) this process is one rank and
+--gpus must equal WORLD_SIZE. Without a launcher, --gpus N > 1 makes this process a
+launcher that starts N rank processes itself (RCCL when every rank has its own GPU,
+gloo when ranks share fewer, stated in config.parallelism). `per_gpu` lists each
+rank's GiB/s and kernel time; `value` = all ranks' bytes / the slowest rank's wall.
+
 value      = algorithmic bytes of all ranks / max-over-ranks wall time, in GiB/s
              (payload + per-packet side arrays + uint16 results)
 roofline   = the dominant (only) kernel's algorithmic bytes / its average launch
@@ -16,24 +22,24 @@ cpu_baseline = the C restatement of checksum.go (oracle/, "port", reference-fait
              same batch (rank 0, N=1 only); the same leg checks the GPU results
              of the timed batch bit-for-bit against it.
 
-Run: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
+Run: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3] [--launch-check]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from yustack_amd import batch  # noqa: E402
-from yustack_amd.shard import max_over_ranks  # noqa: E402
+# numpy / torch / the package are imported by the rank processes only (_imports):
+# the --gpus N launcher must start its N ranks before anything can touch the GPU.
+np = torch = batch = None
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -174,29 +180,40 @@ def timed(w: Workload, steps: int, warmup: int, dist: bool):
     return wall, kern
 
 
-def timed_graph(w: Workload, steps: int, warmup: int):
-    """The same K steps captured once in a HIP graph and replayed (side configs,
-    one rank): a 15-30 us kernel is shorter than a Python-side launch, so eager
-    launches would time the host, not the kernel. Returns (wall s, s per launch)."""
+SIDE_LAUNCHES = 50  # launches per side-config graph, fixed whatever --steps says
+SIDE_SETTLE = 2     # untimed replays first: upload, then ~50 launches of load to leave the clock ramp
+SIDE_TIMED = 3      # timed replays; the per-launch figure is their median
+
+
+def timed_graph(w: Workload, warmup: int):
+    """A side config's launches captured in a HIP graph and replayed: a 15-30 us kernel
+    is shorter than a Python-side launch, so eager launches would time the host, not
+    the kernel. The launch count is fixed (SIDE_LAUNCHES), not tied to --steps: a
+    fresh card needs ~17 ms of sustained load to leave its low-clock ramp (DESIGN.md
+    §5), and 10 launches of a 15-us kernel never get there. Returns (wall s per
+    replay, s per launch), both medians over SIDE_TIMED replays."""
     for k in range(warmup):
         w.step(k)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        for k in range(steps):
+        for k in range(SIDE_LAUNCHES):
             w.step(warmup + k)
-    g.replay()  # first replay uploads the graph
+    for _ in range(SIDE_SETTLE):
+        g.replay()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    g.replay()
-    ev1.record()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kern = ev0.elapsed_time(ev1) / 1e3 / steps
+    walls, kerns = [], []
+    for _ in range(SIDE_TIMED):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record()
+        g.replay()
+        ev1.record()
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+        kerns.append(ev0.elapsed_time(ev1) / 1e3 / SIDE_LAUNCHES)
     del g
-    return wall, kern
+    return sorted(walls)[SIDE_TIMED // 2], sorted(kerns)[SIDE_TIMED // 2]
 
 
 def cpu_baseline(w: Workload, threads: int, budget_s: float):
@@ -341,20 +358,37 @@ def end_to_end(w: Workload, reps: int = 3):
         res[f"tx_burst{bn}_pinned_us_per_call"] = round((time.perf_counter() - t0) / k * 1e6, 1)
     ndev = torch.cuda.device_count()
     if ndev > 1:  # yu_csum_batch_host_uniform_multi: one shard per visible GPU, each on its own PCIe link
-        devs = list(range(ndev))
+        res.update(host_multi(w, list(range(ndev)), pinned, out))
+    return res
+
+
+def host_multi(w: Workload, devs: list, pinned=None, want=None, reps: int = 3) -> dict:
+    """Host memory in and out over several GPUs at once (yu_csum_batch_host_uniform_multi:
+    the batch split into one contiguous shard per listed device, each through that
+    device's own pinned pipeline and PCIe link). Reported beside the
+    device-resident line, never as `value`; never fatal to the bench line."""
+    res, nd = {}, len(devs)
+    try:
+        if pinned is None:
+            pinned = w.data[0].cpu().pin_memory()
+        addrs = None if w.addrs is None else w.addrs.cpu().numpy()
+        init = None if w.initial_arr is None else w.initial_arr.cpu().numpy()
         out2 = np.empty(w.n, np.uint16)
-        try:
+        batch.checksum_host_uniform(pinned, w.L, w.L, w.n, w.mode, initial_arr=init, addrs=addrs,
+                                    out=out2, device=devs)
+        t0 = time.perf_counter()
+        for _ in range(reps):
             batch.checksum_host_uniform(pinned, w.L, w.L, w.n, w.mode, initial_arr=init, addrs=addrs,
                                         out=out2, device=devs)
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                batch.checksum_host_uniform(pinned, w.L, w.L, w.n, w.mode, initial_arr=init, addrs=addrs,
-                                            out=out2, device=devs)
-            dt = (time.perf_counter() - t0) / reps
-            res[f"pinned_{ndev}gpu_GiB_s"] = round(w.bytes / dt / GIB, 2)
-            res[f"pinned_{ndev}gpu_matches"] = bool(np.array_equal(out2, out))
-        except Exception as e:  # reported, never fatal to the bench line
-            res[f"pinned_{ndev}gpu_error"] = str(e)[:200]
+        dt = (time.perf_counter() - t0) / reps
+        res[f"pinned_{nd}gpu_GiB_s"] = round(w.bytes / dt / GIB, 2)
+        if want is None:
+            w.step(0)
+            torch.cuda.synchronize()
+            want = w.out.cpu().numpy()
+        res[f"pinned_{nd}gpu_matches"] = bool(np.array_equal(out2, want))
+    except Exception as e:  # reported, never fatal to the bench line
+        res[f"pinned_{nd}gpu_error"] = str(e)[:200]
     return res
 
 
@@ -376,6 +410,111 @@ def host_threads() -> int:
     return max(1, min(16, n))
 
 
+def _imports():
+    global np, torch, batch
+    import numpy
+    import torch as _torch
+    from yustack_amd import batch as _batch
+    np, torch, batch = numpy, _torch, _batch
+
+
+def _device_count() -> int:
+    """GPUs visible to this process, without initialising HIP (device_count does not
+    on this image; nothing else is called)."""
+    import torch as _torch
+    return _torch.cuda.device_count()
+
+
+def resolve_launch(gpus: int, env: dict, ndev: int) -> dict:
+    """How this process takes part in a --gpus N run (pure; tests/test_bench_launch.py).
+
+    * WORLD_SIZE set (torch.distributed.run started us): we are one rank of it; --gpus
+      must equal WORLD_SIZE, or the line would claim GPUs it never used.
+    * WORLD_SIZE unset, --gpus 1: the single-rank bench.
+    * WORLD_SIZE unset, --gpus N > 1: this process is only a launcher; it starts N rank
+      processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set) before anything here
+      touches a GPU, and exits with their status.
+
+    Backend: RCCL ("nccl") when every rank has a GPU of its own; gloo when ranks share
+    fewer GPUs (a rehearsal on a smaller box: RCCL refuses two ranks on one device).
+    YU_BENCH_BACKEND overrides. Rank r runs on device LOCAL_RANK % ndev."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {gpus})")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        world = int(ws)
+        if world != gpus:
+            raise SystemExit(f"--gpus {gpus} disagrees with WORLD_SIZE={world} from the launcher: "
+                             "pass --gpus equal to --nproc-per-node")
+        role = "rank" if world > 1 else "single"
+        rank, local = int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", env.get("RANK", "0")))
+    else:
+        world, rank, local = gpus, 0, 0
+        role = "spawn" if gpus > 1 else "single"
+    backend = env.get("YU_BENCH_BACKEND") or ("nccl" if ndev >= world else "gloo")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit(f"YU_BENCH_BACKEND must be nccl or gloo (got {backend})")
+    shared = ndev < world
+    return {"role": role, "world": world, "rank": rank, "local": local, "backend": backend,
+            "ndev": ndev, "device": local % max(1, ndev), "shared": shared}
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(plan: dict, argv: list) -> int:
+    """The --gpus N launcher: N child processes running this script as ranks 0..N-1
+    on 127.0.0.1. Nothing in this process has touched a GPU. A rank that fails takes
+    the others down (their exact PIDs); the exit status is the first failure's."""
+    port = _free_port()
+    procs = []
+    for r in range(plan["world"]):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(plan["world"]),
+                   LOCAL_WORLD_SIZE=str(plan["world"]), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   YU_BENCH_BACKEND=plan["backend"])
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                log(f"bench: rank pid {p.pid} exited with {c}; stopping the other ranks")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def launch_check(plan: dict) -> None:
+    """--launch-check: rendezvous and gather each rank's placement, with no GPU work
+    (gloo, whatever the plan's backend), then rank 0 prints it. For CPU tests of the
+    launcher and for checking a node's launch before the real run."""
+    import torch.distributed as dist
+    world = plan["world"]
+    if world > 1:
+        dist.init_process_group("gloo", rank=plan["rank"], world_size=world)
+    me = {"rank": plan["rank"], "local": plan["local"], "device": plan["device"], "pid": os.getpid(),
+          "backend": plan["backend"], "shared": plan["shared"]}
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, me)
+        dist.destroy_process_group()
+    else:
+        ranks = [me]
+    if plan["rank"] == 0:
+        print(json.dumps({"launch_check": {"world": world, "ndev": plan["ndev"], "ranks": ranks}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -383,31 +522,46 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 6, 7, 8, 9, 10, 11])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip configs 2/4 side measurements")
+    ap.add_argument("--no-extra", action="store_true", help="skip the side-config measurements")
     ap.add_argument("--cpu-budget", type=float, default=6.0, help="wall seconds for the CPU baseline")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, rendezvous, print their placement; no GPU work")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    plan = resolve_launch(args.gpus, os.environ, _device_count())
+    if plan["role"] == "spawn":
+        sys.exit(spawn_ranks(plan, sys.argv[1:]))
+    if args.launch_check:
+        launch_check(plan)
+        return
+    rank_main(args, plan)
+
+
+def rank_main(args, plan: dict) -> None:
+    """One rank (or the single process): its own 1M-packet shard of the workload on its
+    own device, timed between barriers; rank 0 prints the line."""
+    _imports()
+    from yustack_amd.shard import gather_over_ranks
+    world, rank, backend = plan["world"], plan["rank"], plan["backend"]
     dist = world > 1
-    # One rank per GPU. YU_BENCH_BACKEND=gloo (rehearsal only) lets several ranks
-    # share fewer GPUs: RCCL refuses two ranks on one device.
-    backend = os.environ.get("YU_BENCH_BACKEND", "nccl")
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    dev = torch.device("cuda", plan["device"])
     torch.cuda.set_device(dev)
     if dist:
         if backend == "nccl":
             torch.distributed.init_process_group("nccl", device_id=dev)
         else:
-            torch.distributed.init_process_group(backend)
+            torch.distributed.init_process_group("gloo")
 
     w = Workload(args.config, dev, seed=1000 + rank)
     wall, kern = timed(w, args.steps, args.warmup, dist)
-    wall_max = max_over_ranks(wall, device=dev if backend == "nccl" else None)
+    # the only collective: each rank's (wall, kernel time, bytes), for the slowest
+    # rank's wall time and the per-GPU figures
+    per = gather_over_ranks([wall, kern, float(w.bytes), float(plan["device"])],
+                            device=dev if dist and backend == "nccl" else None)
+    wall_max = max(p[0] for p in per)
     ms_per_step = wall_max / args.steps * 1e3
-    value = world * w.bytes * args.steps / wall_max / GIB
+    value = sum(p[2] for p in per) * args.steps / wall_max / GIB
     achieved = w.bytes / kern / 1e9  # GB/s (decimal, like the peak)
 
     # HBM bytes per launch from rocprofv3 PMC passes of this same command
@@ -423,6 +577,11 @@ def main():
         except Exception:
             traffic = None
 
+    if backend == "nccl" or not dist:
+        par = f"shard{world} (independent packets, no collective; one rank per GPU)"
+    else:
+        par = (f"shard{world} over gloo, {world} ranks on {plan['ndev']} GPU(s)"
+               + (" — ranks SHARE a card: a launch rehearsal, not a scaling figure" if plan["shared"] else ""))
     res = {
         "metric": "GiB/s device-resident Internet checksum, batched packets, 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -437,15 +596,20 @@ def main():
         "dtype": "u32",
         "data": "synthetic (seeded torch.randint bytes on device; TCP header DataOffset 5, field 0)",
         "config": {
-            "workload": w.name,
+            "workload": w.name + (f"; config5 shape: {world} x 1M packets, one shard per rank" if dist else ""),
             "packets_per_gpu": w.n,
             "packet_bytes": w.L if w.L else "U{64..9000}",
             "mode": {0: "raw", 1: "udp", 2: "tcp", 8: "verify_rx", 9: "tx_datagram"}.get(w.mode, str(w.mode)),
             "algorithmic_bytes_per_step_per_gpu": w.bytes,
             "rotating_batches": w.R,
             "kernel": w.kernel_name(),
-            "parallelism": f"shard{world} (independent packets, no collective)",
+            "parallelism": par,
+            "backend": "rccl" if dist and backend == "nccl" else (backend if dist else "none"),
         },
+        "per_gpu": [{"rank": r, "device": int(p[3]), "GiB_s": round(p[2] * args.steps / p[0] / GIB, 2),
+                     "kernel_avg_us": round(p[1] * 1e6, 2),
+                     "roofline_frac": round(p[2] / p[1] / 1e9 / HBM_PEAK_GBS, 4)}
+                    for r, p in enumerate(per)],
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -465,14 +629,14 @@ def main():
             if c == args.config:
                 continue
             wc = Workload(c, dev, seed=77 + c)
-            ks = max(10, args.steps // 2)
-            wl, kc = timed_graph(wc, ks, args.warmup)
+            wl, kc = timed_graph(wc, args.warmup)
             extra[f"config{c}"] = {
-                "GiB_s": round(wc.bytes * ks / wl / GIB, 2),
+                "GiB_s": round(wc.bytes * SIDE_LAUNCHES / wl / GIB, 2),
                 "kernel_avg_us": round(kc * 1e6, 2),
                 "roofline_frac": round(wc.bytes / kc / 1e9 / HBM_PEAK_GBS, 4),
                 "kernel": wc.kernel_name(),
-                "timing": f"{ks} launches captured in one HIP graph, replayed once",
+                "timing": (f"{SIDE_LAUNCHES} launches captured in one HIP graph; {SIDE_SETTLE} untimed "
+                           f"replays, median of {SIDE_TIMED} timed replays"),
             }
             del wc
             torch.cuda.empty_cache()
@@ -480,6 +644,9 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_e2e:
         res["end_to_end_host_memory"] = end_to_end(w)
+    if rank == 0 and dist and not args.no_e2e and plan["ndev"] >= world:
+        # host memory over all the job's GPUs at once, on rank 0 after the timed region
+        res["end_to_end_host_memory"] = host_multi(w, list(range(world)))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         parity, cb = cpu_baseline(w, host_threads(), args.cpu_budget)

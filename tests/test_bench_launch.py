@@ -1,0 +1,87 @@
+"""bench.py's --gpus N launch on CPU: argument resolution (pure) and the self-launch
+of N rank processes that rendezvous over gloo (``--launch-check``: no GPU work).
+The timed path itself is GPU-only (tests/test_gpu_dist.py runs it on one card)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402  (stdlib-only at import: the launcher touches no GPU)
+
+
+def test_bench_import_is_stdlib_only():
+    assert bench.np is None and bench.torch is None and bench.batch is None
+
+
+def test_single_process_default():
+    p = bench.resolve_launch(1, {}, 1)
+    assert p["role"] == "single" and p["world"] == 1 and p["device"] == 0 and p["backend"] == "nccl"
+
+
+def test_gpus_n_without_launcher_spawns():
+    p = bench.resolve_launch(8, {}, 8)
+    assert p["role"] == "spawn" and p["world"] == 8 and p["backend"] == "nccl" and not p["shared"]
+    p = bench.resolve_launch(2, {}, 1)  # one card: ranks share it over gloo
+    assert p["role"] == "spawn" and p["backend"] == "gloo" and p["shared"]
+
+
+def test_rank_under_torchrun():
+    env = {"WORLD_SIZE": "4", "RANK": "3", "LOCAL_RANK": "3"}
+    p = bench.resolve_launch(4, env, 8)
+    assert (p["role"], p["world"], p["rank"], p["device"], p["backend"]) == ("rank", 4, 3, 3, "nccl")
+    p = bench.resolve_launch(4, env, 2)
+    assert p["device"] == 1 and p["backend"] == "gloo" and p["shared"]
+    p = bench.resolve_launch(1, {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, 1)
+    assert p["role"] == "single"
+
+
+def test_gpus_disagreeing_with_world_size_fails_loudly():
+    with pytest.raises(SystemExit, match="disagrees"):
+        bench.resolve_launch(8, {"WORLD_SIZE": "2", "RANK": "0"}, 8)
+    with pytest.raises(SystemExit):
+        bench.resolve_launch(0, {}, 1)
+    with pytest.raises(SystemExit, match="YU_BENCH_BACKEND"):
+        bench.resolve_launch(2, {"YU_BENCH_BACKEND": "mpi"}, 2)
+
+
+def test_backend_override():
+    assert bench.resolve_launch(2, {"YU_BENCH_BACKEND": "gloo"}, 8)["backend"] == "gloo"
+
+
+def _run(args, env=None, timeout=240):
+    e = dict(os.environ, **(env or {}))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "YU_BENCH_BACKEND"):
+        if env is None or k not in env:
+            e.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=e,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_self_launch_starts_n_ranks(n):
+    r = _run(["--gpus", str(n), "--launch-check"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 alone prints
+    lc = json.loads(lines[0])["launch_check"]
+    assert lc["world"] == n
+    assert [x["rank"] for x in lc["ranks"]] == list(range(n))
+    assert [x["local"] for x in lc["ranks"]] == list(range(n))
+    assert len({x["pid"] for x in lc["ranks"]}) == n
+    assert all(x["backend"] == "gloo" and x["shared"] for x in lc["ranks"])  # no GPU in this container
+
+
+def test_mismatch_exits_nonzero():
+    r = _run(["--gpus", "4", "--launch-check"], env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0 and "disagrees" in r.stderr
+
+
+def test_failing_rank_fails_the_launch():
+    # no GPU here: every rank fails at its device; the launcher must not report success
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-extra", "--no-e2e", "--no-cpu-baseline"])
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -1,0 +1,135 @@
+"""Multi-rank product path on one MI355X: ranks share cuda:0 over gloo,
+each runs the HIP path (batch.checksum_uniform / checksum_ragged through the C ABI)
+on its own shard (yustack_amd.shard), and rank 0 checks that the shards' results,
+concatenated, equal the oracle's over the whole batch. Shards are re-based to start
+at byte 0 on their rank, as a real split hands them over, so alignments change.
+Plus bench.py --gpus 2 self-launching two ranks on the one card."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batches():
+    """Seeded on every rank alike: a config-3-shaped uniform TCP batch, a
+    config-4-shaped ragged RAW batch and a config-6-shaped VERIFY_RX batch (sizes
+    cut so the oracle finishes in seconds; each rank's shard still crosses the
+    k_small run and 16-packet k_seg cut-overs)."""
+    rng = np.random.default_rng(2024)
+    n3, L = 200003, 1500
+    b3 = rng.integers(0, 256, size=n3 * L, dtype=np.uint8)
+    b3.reshape(n3, L)[:, 12] = 0x50
+    b3.reshape(n3, L)[:, 16:18] = 0
+    a3 = rng.integers(0, 256, size=8 * n3, dtype=np.uint8)
+    n4 = 100001
+    l4 = rng.integers(64, 9001, size=n4)
+    o4 = np.zeros(n4 + 1, np.int64)
+    o4[1:] = np.cumsum(l4)
+    b4 = rng.integers(0, 256, size=int(o4[-1]), dtype=np.uint8)
+    i4 = rng.integers(0, 65536, size=n4, dtype=np.uint16)
+    n6 = 150001
+    l6 = rng.integers(40, 1501, size=n6)
+    o6 = np.zeros(n6 + 1, np.int64)
+    o6[1:] = np.cumsum(l6)
+    b6 = rng.integers(0, 256, size=int(o6[-1]), dtype=np.uint8)
+    s6 = o6[:-1]
+    b6[s6], b6[s6 + 2], b6[s6 + 3], b6[s6 + 9] = 0x45, l6 >> 8, l6 & 0xFF, 6
+    return (n3, L, b3, a3), (o4, b4, i4), (o6, b6)
+
+
+def _rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from yustack_amd import batch
+    from yustack_amd.shard import gather_over_ranks, shard_ragged, shard_uniform
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        (n3, L, b3, a3), (o4, b4, i4), (o6, b6) = _batches()
+        mine = {}
+        f, c = shard_uniform(n3, world, rank)
+        d = torch.from_numpy(b3[f * L:(f + c) * L].copy()).to(dev)
+        a = torch.from_numpy(a3[8 * f:8 * (f + c)].copy()).to(dev)
+        mine["tcp"] = batch.checksum_uniform(d, L, L, c, "tcp", addrs=a).cpu().numpy().tolist()
+        mine["tcp_kernel"] = batch.variant(L, L, "tcp", d.data_ptr() & 15, n=c)
+        for name, (o, b, ia, mode) in (("raw", (o4, b4, i4, "raw")), ("rx", (o6, b6, None, "verify_rx"))):
+            f, c = shard_ragged(o, world, rank)
+            lo, hi = int(o[f]), int(o[f + c])
+            d = torch.from_numpy(b[lo:hi].copy()).to(dev)
+            offs = torch.from_numpy(o[f:f + c + 1] - lo).to(dev)
+            ini = None if ia is None else torch.from_numpy(ia[f:f + c].copy()).to(dev)
+            mine[name] = batch.checksum_ragged(d, offs, mode, initial_arr=ini).cpu().numpy().tolist()
+            mine[name + "_kernel"] = batch.ragged_variant(mode, c)
+        torch.cuda.synchronize()
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)  # test-only gather of the results
+        per = gather_over_ranks([rank, 2.0 * rank])
+        if rank == 0:
+            from oracle import oracle as O
+            C = O.C()
+            ok = {}
+            want = C.batch(b3, O.MODE_TCP, stride=L, length=L, n=n3, addrs=a3, threads=8)
+            ok["tcp"] = sum((p["tcp"] for p in parts), []) == want.tolist()
+            want = C.batch(b4, O.MODE_RAW, offsets=o4.view(np.uint64), initial_arr=i4, threads=8)
+            ok["raw"] = sum((p["raw"] for p in parts), []) == want.tolist()
+            want = C.batch(b6, O.MODE_VERIFY_RX, offsets=o6.view(np.uint64), threads=8)
+            ok["rx"] = sum((p["rx"] for p in parts), []) == want.tolist()
+            q.put((ok, [[p[k] for k in ("tcp_kernel", "raw_kernel", "rx_kernel")] for p in parts], per))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shards_on_hip_path_concatenate_to_oracle(dev, world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        ok, kernels, per = q.get(timeout=180)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert ok == {"tcp": True, "raw": True, "rx": True}, (ok, kernels)
+    assert per == [[r, 2.0 * r] for r in range(world)]
+    assert all(p.exitcode == 0 for p in procs)
+    # every rank ran the device kernels, not a host path
+    assert all(k[0].startswith("k_") for k in kernels)
+
+
+def test_bench_self_launch_two_ranks_on_one_card(dev):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "YU_BENCH_BACKEND")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "10",
+                        "--warmup", "2", "--no-extra", "--no-e2e", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and len(line["per_gpu"]) == 2
+    assert [p["rank"] for p in line["per_gpu"]] == [0, 1]
+    assert all(p["GiB_s"] > 0 and p["kernel_avg_us"] > 0 for p in line["per_gpu"])
+    assert line["config"]["backend"] == "gloo" and "SHARE" in line["config"]["parallelism"]
+    assert line["config"]["kernel"] == "k_small<16,6>"

@@ -5,8 +5,9 @@ batch shards across the GPUs of a node with no data-path collective: contiguous
 packet ranges, one rank per GPU. Uniform batches split evenly by packet count;
 ragged batches split on packet boundaries balanced by bytes (a prefix-sum search),
 since 64..9000-byte packets make equal counts very unequal in work. The only
-communication is the control-plane timing reduction (:func:`max_over_ranks`) that
-bench.py uses to report the slowest rank.
+communication is control-plane timing (:func:`gather_over_ranks`, one all_gather of
+each rank's wall and kernel time) that bench.py uses to report the slowest rank and
+the per-GPU rates.
 """
 from __future__ import annotations
 
@@ -51,3 +52,20 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_over_ranks(values, device=None) -> list[list[float]]:
+    """Every rank's list of floats (same length on all ranks), in rank order: one
+    all_gather of a small float64 tensor over the default group (RCCL when
+    ``device`` is a GPU, gloo for CPU tensors). ``[values]`` when torch.distributed
+    is not initialised. bench.py uses it for the per-GPU figures and the slowest
+    rank's wall time; it never carries packet data."""
+    import torch
+    import torch.distributed as dist
+    vals = [float(v) for v in values]
+    if not (dist.is_available() and dist.is_initialized()):
+        return [vals]
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [p.cpu().tolist() for p in parts]
