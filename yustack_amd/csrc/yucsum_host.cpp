@@ -380,7 +380,8 @@ template <class Layout>
 int run_slices(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
                const uint8_t *h_addrs, uint16_t *h_out, bool pin_out) {
   int rc = YU_OK;
-  uint64_t k = 0;
+  const uint64_t outs = YU_MODE_OUTPUTS(L.mode);  // results per packet
+  uint64_t k = 0;                                 // slice counter: slot k % kSlots
   for (uint64_t first = 0; first < n; ++k) {
     Slot &x = c.s[k % kSlots];
     rc = finish(x, h_out);
@@ -406,10 +407,9 @@ int run_slices(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
     rc = L.launch(x.d_data, x.d_off, cnt, d_init, d_addrs, x.d_out, x.st);
     if (rc) return rc;
     x.staged_out = !pin_out;
-    const uint64_t k = YU_MODE_OUTPUTS(L.mode);
-    YU_TRY(hipMemcpyAsync(pin_out ? h_out + first * k : x.h_out, x.d_out, cnt * 2 * k,
+    YU_TRY(hipMemcpyAsync(pin_out ? h_out + first * outs : x.h_out, x.d_out, cnt * 2 * outs,
                           hipMemcpyDeviceToHost, x.st));
-    x.outs = k;
+    x.outs = outs;
     YU_TRY(hipEventRecord(x.done, x.st));
     x.first = first;
     x.cnt = cnt;
@@ -823,19 +823,11 @@ extern "C" int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t 
 // ---------------------------------------------------------------------
 namespace {
 
-bool tx_mode(int m) {
-  return m == YU_MODE_UDP || m == YU_MODE_TCP || m == YU_MODE_IPV4 || m == YU_MODE_ICMP ||
-         m == YU_MODE_TX_DATAGRAM;
-}
+using yu::l4_field;  // the kernels' protocol tables (yucsum_internal.h)
+using yu::l4_min;
+using yu::mode_field;
 
-uint32_t field_offset(int m) {
-  switch (m) {
-    case YU_MODE_UDP: return 6;
-    case YU_MODE_TCP: return 16;
-    case YU_MODE_IPV4: return 10;
-    default: return 2;  // ICMP
-  }
-}
+bool tx_mode(int m) { return yu::mode_fills(m); }
 
 // Byte k of packet i, through a layout's accessor (nullptr past the packet).
 // set(i) writes packet i's field; the packets are split over the copy pool.
@@ -859,14 +851,13 @@ void put_datagram_fields(const At &at, uint64_t i, const uint16_t *res) {
   if (hl < 20u || hl > tl || !at(i, tl - 1u)) return;
   put_field(at, i, 10, res[2 * i]);
   const uint32_t proto = *b9;
-  const uint32_t fo = proto == 17 ? 6 : (proto == 6 ? 16 : (proto == 1 ? 2 : 0));
-  const uint32_t mn = proto == 17 ? 8 : (proto == 6 ? 20 : 4);
-  if (fo && tl - hl >= mn) put_field(at, i, hl + fo, res[2 * i + 1]);
+  const uint32_t fo = l4_field(proto);
+  if (fo && tl - hl >= l4_min(proto)) put_field(at, i, hl + fo, res[2 * i + 1]);
 }
 
 template <class At>
 void set_fields(uint64_t n, int mode, const uint16_t *res, const At &at) {
-  const uint32_t f = field_offset(mode);
+  const uint32_t f = mode_field(mode);
   auto one = [&](uint64_t i) {
     if (mode == YU_MODE_TX_DATAGRAM) {
       put_datagram_fields(at, i, res);

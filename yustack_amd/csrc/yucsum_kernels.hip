@@ -108,41 +108,17 @@ struct BatchArgs {
 __host__ __device__ __forceinline__ bool mode_is_ipv4(int m) {
   return m == YU_MODE_IPV4 || m == YU_MODE_VERIFY_IPV4;
 }
-__host__ __device__ __forceinline__ bool mode_is_tx(int m) {
-  return m == YU_MODE_UDP || m == YU_MODE_TCP || m == YU_MODE_IPV4 ||
-         m == YU_MODE_ICMP;
-}
-// Modes that may write in place (the single-field TX modes and TX_DATAGRAM).
-__host__ __device__ __forceinline__ bool mode_fills(int m) {
-  return mode_is_tx(m) || m == YU_MODE_TX_DATAGRAM;
-}
-// Offset of the transport checksum field in a segment of IPv4 protocol
-// `proto`, and the segment's minimum length (UDP 6/8, TCP 16/20, ICMP 2/4);
-// 0 / 0 for other protocols.
-__host__ __device__ __forceinline__ uint32_t l4_field(uint32_t proto) {
-  return proto == 17u ? 6u : (proto == 6u ? 16u : (proto == 1u ? 2u : 0u));
-}
-__host__ __device__ __forceinline__ uint32_t l4_min(uint32_t proto) {
-  return proto == 17u ? 8u : (proto == 6u ? 20u : (proto == 1u ? 4u : 0u));
-}
+using yu::l4_field;  // protocol tables shared with the host writer (yucsum_internal.h)
+using yu::l4_min;
+using yu::mode_field;
+using yu::mode_fills;
+using yu::mode_is_tx;
 __host__ __device__ __forceinline__ bool mode_has_pseudo(int m) {
   return m == YU_MODE_UDP || m == YU_MODE_TCP || m == YU_MODE_VERIFY_TCP ||
          m == YU_MODE_VERIFY_UDP;
 }
 __host__ __device__ __forceinline__ uint32_t mode_proto(int m) {
   return (m == YU_MODE_TCP || m == YU_MODE_VERIFY_TCP) ? 6u : 17u;
-}
-// Offset of the checksum field a TX mode takes as zero
-// (header/udp.go udpChecksum=6, header/tcp.go tcpChecksum=16,
-//  header/ipv4.go ipChecksum=10, header/icmpv4.go checksum at 2).
-__host__ __device__ __forceinline__ uint32_t mode_field(int m) {
-  switch (m) {
-    case YU_MODE_UDP: return 6;
-    case YU_MODE_TCP: return 16;
-    case YU_MODE_IPV4: return 10;
-    case YU_MODE_ICMP: return 2;
-    default: return 0;
-  }
 }
 __host__ __device__ __forceinline__ uint32_t min_len(int m) {
   switch (m) {
@@ -2025,9 +2001,9 @@ struct Variant {
   uint32_t ppw;     // packets per wave step
   KernelFn fill = nullptr;  // in-place fill instantiation, if it has its own
   uint32_t run = 0;  // packets per wave run (k_small), 0 = ppw
-  // k_small without runs (PR = 0): the in-place fill, and batches too small to
-  // give every wave of the grid a whole run
-  KernelFn inter = nullptr;
+  // k_small without runs (PR = 0), by load policy like fn: the in-place fill,
+  // and batches too small to give every wave of the grid a whole run
+  KernelFn inter[3] = {nullptr, nullptr, nullptr};
 };
 
 // k_small runs of 16 packets per wave (one side-record load and one result
@@ -2041,7 +2017,8 @@ constexpr int kSmallRun = 16;
 #define YU_SMALL(G, U)                                                                     \
   {"k_small<" #G "," #U ">", 16u * G * U,                                                  \
    {k_small<G, U, 0, kSmallRun>, k_small<G, U, 1, kSmallRun>, k_small<G, U, 2, kSmallRun>}, \
-   G, 64u / G, nullptr, kSmallRun, k_small<G, U, 2, 0>}
+   G, 64u / G, nullptr, kSmallRun,                                                         \
+   {k_small<G, U, 0, 0>, k_small<G, U, 1, 0>, k_small<G, U, 2, 0>}}
 #define YU_TINY(G, FILL) \
   {"k_tiny<" #G ">", 16u * G, {k_tiny<G, 0>, k_tiny<G, 1>, k_tiny<G, 1>}, G, 64u, FILL}
 
@@ -2302,7 +2279,7 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   a.xcd = (uint32_t)use_xcd();
   a.small_waves = (uint32_t)cu_count(dev) * 4u * (uint32_t)seg_small_blocks();
   KernelFn k = A.fill && v.fill ? v.fill : v.fn[use_nt()];
-  if (v.run && !runs) k = v.inter;
+  if (v.run && !runs) k = v.inter[use_nt()];
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
