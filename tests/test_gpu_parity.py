@@ -971,6 +971,38 @@ def test_k_small_runs_at_grid_size(dev, oracle_c, stride, length, mode, align, n
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
 
 
+@pytest.mark.parametrize("stride,length,mode,align,n,kern", [
+    (3604, 3501, "raw", 0, 40000 + 5, "k_small<64,4>"),   # GPW 1, SPR 16: shfl src = step, lane 63 finishes
+    (3602, 3600, "udp", 2, 32768 + 9, "k_small<64,4>"),
+    (704, 700, "tcp", 0, 40000 + 3, "k_small<16,3>"),
+    (1000, 1000, "raw", 3, 40000 + 11, "k_small<16,4>"),
+    (3000, 2900, "udp", 0, 40000 + 1, "k_small<32,6>"),
+])
+def test_k_small_runs_every_shape(dev, oracle_c, stride, length, mode, align, n, kern):
+    """The run mapping (16 consecutive packets per wave) in the k_small shapes the
+    grid-size test does not reach: k_small<64,4> (one packet per wave step, so a
+    run is 16 steps and the result of step k comes from lane 63 to lane k) and
+    <16,3>, <16,4>, <32,6>; batches past 8 runs per CU (so runs apply) with a
+    partial last run, initial arrays or address records, unaligned starts."""
+    mod = {"raw": O.MODE_RAW, "udp": O.MODE_UDP, "tcp": O.MODE_TCP}[mode]
+    assert batch.variant(stride, length, mode, align, n=n) == kern
+    assert n // 16 >= 8 * torch.cuda.get_device_properties(dev).multi_processor_count and n % 16
+    g = torch.Generator(device=dev)
+    g.manual_seed(n * 3 + stride)
+    total = align + (n - 1) * stride + length
+    d = torch.randint(0, 256, (total + 16,), dtype=torch.uint8, device=dev, generator=g)
+    if mode == "tcp":
+        d[align + 12: align + 12 + (n - 1) * stride + 1: stride] = 0x50
+    ia = torch.randint(0, 1 << 16, (n,), dtype=torch.int32, device=dev, generator=g).to(torch.uint16) \
+        if mode == "raw" else None
+    ad = torch.randint(0, 256, (8 * n,), dtype=torch.uint8, device=dev, generator=g) if mode != "raw" else None
+    got = batch.checksum_uniform(d[align:], stride, length, n, mode, initial_arr=ia, addrs=ad).cpu().numpy()
+    want = oracle_c.batch(d.cpu().numpy()[align:], mod, stride=stride, length=length, n=n,
+                          initial_arr=None if ia is None else ia.cpu().numpy(),
+                          addrs=None if ad is None else ad.cpu().numpy(), threads=8)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
 @pytest.mark.parametrize("mode", ["tcp", "udp"])
 @pytest.mark.parametrize("length,gap,n", [
     (1280, 0, 40000 + 3), (1281, 3, 40000 + 5), (1283, 1, 33000 + 1), (1390, 2, 40000 + 15),
