@@ -410,6 +410,21 @@ def host_threads() -> int:
     return max(1, min(16, n))
 
 
+def pmc_traffic(cfg: int, kernel: str):
+    """HBM bytes per launch of config `cfg` from rocprofv3 PMC passes of this same
+    command (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from
+    tools/profile.sh output: 2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes), if the
+    record is for the kernel this run launches; else (None, None)."""
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        rec = json.load(open(tf)).get(f"config{cfg}")
+        if rec and rec.get("kernel") == kernel:
+            return rec["hbm_bytes_per_launch"], rec["source"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None, None
+
+
 def _imports():
     global np, torch, batch
     import numpy
@@ -564,18 +579,7 @@ def rank_main(args, plan: dict) -> None:
     value = sum(p[2] for p in per) * args.steps / wall_max / GIB
     achieved = w.bytes / kern / 1e9  # GB/s (decimal, like the peak)
 
-    # HBM bytes per launch from rocprofv3 PMC passes of this same command
-    # (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from
-    # tools/profile.sh output: 2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes).
-    traffic, traffic_src = None, None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            rec = json.load(open(tf)).get(f"config{args.config}")
-            if rec and rec.get("kernel") == w.kernel_name():
-                traffic, traffic_src = rec["hbm_bytes_per_launch"], rec["source"]
-        except Exception:
-            traffic = None
+    traffic, traffic_src = pmc_traffic(args.config, w.kernel_name())
 
     if backend == "nccl" or not dist:
         par = f"shard{world} (independent packets, no collective; one rank per GPU)"
@@ -638,6 +642,10 @@ def rank_main(args, plan: dict) -> None:
                 "timing": (f"{SIDE_LAUNCHES} launches captured in one HIP graph; {SIDE_SETTLE} untimed "
                            f"replays, median of {SIDE_TIMED} timed replays"),
             }
+            tr, _ = pmc_traffic(c, wc.kernel_name())
+            if tr:  # bytes the kernel physically moves (PMC): the in-place writers write whole ranges
+                extra[f"config{c}"]["traffic_bytes"] = tr
+                extra[f"config{c}"]["traffic_frac"] = round(tr / kc / 1e9 / HBM_PEAK_GBS, 4)
             del wc
             torch.cuda.empty_cache()
         res["other_configs"] = extra

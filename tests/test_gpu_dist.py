@@ -133,3 +133,37 @@ def test_bench_self_launch_two_ranks_on_one_card(dev):
     assert all(p["GiB_s"] > 0 and p["kernel_avg_us"] > 0 for p in line["per_gpu"])
     assert line["config"]["backend"] == "gloo" and "SHARE" in line["config"]["parallelism"]
     assert line["config"]["kernel"] == "k_small<16,6>"
+
+
+def _rccl_rank(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from yustack_amd.shard import gather_over_ranks, max_over_ranks
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        per = gather_over_ranks([1.5, 2.5, 3.0], device=dev)
+        mx = max_over_ranks(4.25, device=dev)
+        q.put((per, mx, dist.get_backend()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_timing_collectives_one_rank(dev):
+    """The RCCL ("nccl") group bench.py builds when every rank has its own GPU, at
+    world size 1 (the box has one card; RCCL refuses two ranks on one device):
+    the per-GPU gather and the max over ranks run on device tensors."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_rank, args=(_free_port(), q))
+    p.start()
+    try:
+        per, mx, backend = q.get(timeout=120)
+    finally:
+        p.join(timeout=60)
+    assert per == [[1.5, 2.5, 3.0]] and mx == 4.25 and backend == "nccl"
+    assert p.exitcode == 0
