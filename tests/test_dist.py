@@ -1,6 +1,8 @@
-"""Multi-rank path on CPU (gloo, world_size 2): packet shards, per-rank results and
-the max-over-ranks timing reduction bench.py uses. Packets are independent, so
-the shards' results concatenated equal the whole batch's — no data collective."""
+"""Multi-rank plumbing on CPU (gloo, world_size 2): the shard arithmetic of
+yustack_amd.shard and the timing collectives bench.py uses (gather_over_ranks,
+max_over_ranks). The shards here run the oracle, so this checks the split, not the
+product: the HIP path on shards is tests/test_gpu_dist.py. Packets are independent,
+so the shards' results concatenated equal the whole batch's — no data collective."""
 import os
 import socket
 
@@ -9,7 +11,7 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from yustack_amd.shard import max_over_ranks, shard_ragged, shard_uniform
+from yustack_amd.shard import gather_over_ranks, max_over_ranks, shard_ragged, shard_uniform
 
 
 def test_shard_uniform_covers_exactly():
@@ -61,9 +63,11 @@ def _worker(rank, world, port, q):
         parts = [None] * world
         dist.all_gather_object(parts, part.tolist())  # test-only gather of results
         t = max_over_ranks(0.5 + rank)
+        per = gather_over_ranks([rank, cnt])
         if rank == 0:
             full = O.C().batch(host, O.MODE_TCP, stride=L, length=L, n=n, addrs=addrs)
-            q.put((sum(parts, []) == full.tolist(), t, torch.__version__ is not None))
+            ok = sum(parts, []) == full.tolist() and per == [[0.0, n / 2], [1.0, n / 2]]
+            q.put((ok, t, torch.__version__ is not None))
     finally:
         dist.destroy_process_group()
 
