@@ -77,6 +77,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "yucsum.h"
 #include "yucsum_internal.h"
@@ -1444,8 +1445,9 @@ __device__ __forceinline__ uint32_t seg_part(const uint4 &d, uint32_t r) {
 
 // One point of a lane: position x (relative to b0), and P / T at x once the
 // tile holding x has gone by.
+template <typename Pos>
 struct SegPt {
-  uint64_t x;
+  Pos x;
   uint32_t p, t;
 };
 
@@ -1583,7 +1585,13 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   const uint64_t end = A.offsets ? data + A.offsets[A.n] : A.end;
   const uint32_t *s_dw = (const uint32_t *)s_data[wid];
   const bool contig = A.offsets != nullptr;  // ragged: packets back to back
-  constexpr uint64_t kNoPt = ~0ull;          // a point slot not in use
+  // Positions relative to the chunk's b0: 64-bit for the plain kind (RAW packets
+  // up to YU_MAX_RAW_LEN), 32-bit for the TX / RX / DG kinds, whose packets are
+  // at most 65535 bytes (include/yucsum.h), so a 64-packet chunk spans < 4.2 MB
+  // (uniform batches with sparser strides take k_loop_rx, pick_uniform). Half the
+  // VALU work on every point test and offset.
+  using Pos = typename std::conditional<K == kSegPlain, uint64_t, uint32_t>::type;
+  constexpr Pos kNoPt = ~(Pos)0;             // a point slot not in use
 
   uint64_t ch = wave;
   if (wave >= nwave || ch * CH >= A.n) return;
@@ -1593,20 +1601,20 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   seg_geom(data, A.n, ch * CH, cur);
 
   // per-chunk state
-  SegPt pt[4];  // start, end, then (RX, DG) header and transport end
+  SegPt<Pos> pt[4];  // start, end, then (RX, DG) header and transport end
   SegRx rx;
   // TX, DG: the checksum field's next unread byte (kNoPt: none or done; DG: the
   // transport field), the bytes of it still to read (2, or 1 when the field
   // straddles two tiles) and the address-ordered LE sum of those read:
   // P(field end) - P(field start) without two more point evaluations per tile
-  uint64_t fx = 0;
+  Pos fx = 0;
   uint32_t fk = 0, fsum = 0;
   bool exact = false;
   uint32_t carry_l = 0, carry_t = 0;
   auto begin_chunk = [&](const SegChunk &k) __attribute__((always_inline)) {
-    const uint64_t x = data + k.ox - k.b0;
-    const uint64_t y = data + k.oy - k.b0;
-    const uint64_t len = y - x;
+    const Pos x = (Pos)(data + k.ox - k.b0);
+    const Pos y = (Pos)(data + k.oy - k.b0);
+    const uint64_t len = k.oy - k.ox;
     pt[0].x = x;
     // ragged packets lie back to back: P(end) is the next lane's P(start), so
     // only lane 63 evaluates an end point (the chunk end); RX needs none
@@ -1654,7 +1662,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
                           end, cn);
 
     // chunk sums, address-ordered exclusive prefixes (DPP scan per u)
-    const uint64_t tb = t * T;
+    const Pos tb = (Pos)(t * T);
     uint32_t pl[U], ptt[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1680,7 +1688,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
     for (int i = 0; i < NP; ++i) here |= pt[i].x - tb < T;
     if (FB) here |= fx - tb < T;
     if (RX) {  // a header window [floor4(start), +24) still being gathered
-      const uint64_t hs = pt[0].x & ~3ull;
+      const Pos hs = pt[0].x & ~(Pos)3;
       here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
     }
     if (__any((int)here)) {  // a packet boundary (or header) lies in this tile
@@ -1692,12 +1700,22 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
       __builtin_amdgcn_wave_barrier();
       bool parsed = false;
       if (RX && rx.need) {  // gather header dwords held by this tile, parse
+        const Pos q0 = (pt[0].x & ~(Pos)3) - tb;
+        if (q0 <= (Pos)(T - 24u)) {
+          // the whole 24-byte window lies in this tile (q0 wraps past T when
+          // the window began in an earlier one): six reads, no bookkeeping
+          const uint32_t d = (uint32_t)q0 >> 2;
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-          const uint64_t q = (pt[0].x & ~3ull) + 4u * (uint32_t)j - tb;
-          if (((rx.need >> j) & 1u) && q < T) {
-            rx.h[j] = s_dw[(uint32_t)q >> 2];
-            rx.need &= ~(1u << j);
+          for (int j = 0; j < 6; ++j) rx.h[j] = s_dw[d + (uint32_t)j];
+          rx.need = 0u;
+        } else {  // a window across two tiles: the dwords this one holds
+#pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            const Pos q = q0 + 4u * (uint32_t)j;
+            if (((rx.need >> j) & 1u) && q < T) {
+              rx.h[j] = s_dw[(uint32_t)q >> 2];
+              rx.need &= ~(1u << j);
+            }
           }
         }
         if (rx.need == 0u) {
@@ -1724,14 +1742,14 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
       }
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
-        const uint64_t q = pt[i].x - tb;
+        const Pos q = pt[i].x - tb;
         if (q < T) {
           const uint32_t k = (uint32_t)q >> 4;
           pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
         }
       }
       if (FB) {  // the field's bytes, weighted by address parity
-        const uint64_t q = fx - tb;
+        const Pos q = fx - tb;
         if (q < T) {
           const uint8_t *sb = (const uint8_t *)s_data[wid];
           const uint32_t b = sb[q];
@@ -1771,7 +1789,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
-          const uint64_t q = pt[i].x - tb;
+          const Pos q = pt[i].x - tb;
           if (q < T) {
             const uint32_t k = (uint32_t)q >> 4;
             pt[i].t = s_pre[wid][k] + seg_part<true>(s_data[wid][k], (uint32_t)q & 15u);
@@ -2089,6 +2107,9 @@ const Variant &seg_for(bool u8, int mode) {
 // from 16384 packets on k_seg wins on small packets (5.4 vs 11.5). VERIFY_RX
 // bursts take k_loop_rx, the same shape.
 constexpr uint64_t kSmallBurst = 4096;
+// the largest uniform stride k_seg's 32-bit kinds take: 63 strides plus a 65535-byte
+// packet and its 3 head bytes stay under 2^31 bytes
+constexpr uint64_t kSeg32Stride = ((1ull << 31) - 65535u - 3u) / 63u;
 constexpr uint64_t kMidBatch = 65536;
 
 const Variant &pick_ragged(int mode, uint64_t n) {
@@ -2137,12 +2158,18 @@ const Variant &pick_uniform(uint64_t base, uint64_t stride, uint32_t len,
     return tiny_ok && (stride & 3u) == 0 && len >= 1u && len <= stride && stride <= v.window &&
            2u * stride <= 3u * (uint64_t)len;
   };
-  if (mode == YU_MODE_VERIFY_RX || mode == YU_MODE_TX_DATAGRAM) return pick_ragged(mode, n);
+  if (mode == YU_MODE_VERIFY_RX || mode == YU_MODE_TX_DATAGRAM) {
+    // k_seg's RX / DG kinds keep positions in 32 bits: a 64-packet chunk must
+    // span less than 2 GiB, so sparser uniform batches take a wave per datagram
+    if (n > 1 && stride > kSeg32Stride) return mode == YU_MODE_VERIFY_RX ? kLoopRx : kLoopDg;
+    return pick_ragged(mode, n);
+  }
   // IPv4 header-only modes: one lane per packet (1M x 1500-B datagrams:
   // 29.9 us vs 36.9 with k_small<4,1>, kbench 13)
   if (mode_is_ipv4(mode) && !forced_variant()) return kHdr;
   if (const char *f = forced_variant()) {
-    if (!mode_is_ipv4(mode) && strncmp(f, "k_seg<", 6) == 0) return seg_for(f[6] == '8', mode);
+    if (!mode_is_ipv4(mode) && strncmp(f, "k_seg<", 6) == 0 && (n < 2 || stride <= kSeg32Stride))
+      return seg_for(f[6] == '8', mode);
     if (mode_is_ipv4(mode) && strcmp(f, kHdr.name) == 0) return kHdr;
     for (const Variant &v : kSmall)
       if (strcmp(v.name, f) == 0 && fits(v)) return v;
