@@ -1467,6 +1467,8 @@ struct SegRx {
   uint32_t fo;      // TX_DATAGRAM: transport field offset in the packet (0: none)
   uint32_t h20;     // k_seg: the header is the plain 20 bytes (IHL 5) of a valid packet
   uint32_t hsum;    // k_seg: then the address-ordered LE sum of those 20 bytes
+  uint32_t tnext;   // k_seg, ragged: TotalLength() == len, so the transport end is
+                    // the next lane's start point (no point of its own)
 };
 
 // TX_DATAGRAM on a parsed header (rx_parse): the datagram is in contract when
@@ -1479,7 +1481,7 @@ struct SegRx {
 __device__ __forceinline__ uint32_t dg_parse(SegRx &rx, uint32_t sh, uint32_t hl, uint32_t tl) {
   const bool ok = !(rx.flags & YU_RX_INVALID) && hl >= 20u;
   rx.hl = ok ? hl : 0u;
-  const uint32_t w2 = sh ? __builtin_amdgcn_alignbyte(rx.h[3], rx.h[2], sh) : rx.h[2];  // bytes 8..11
+  const uint32_t w2 = __builtin_amdgcn_alignbyte(rx.h[3], rx.h[2], sh);  // bytes 8..11 (sh 0: h[2])
   const uint32_t f = w2 >> 16;
   rx.ipf = (sh & 1u) ? ((f >> 8) | ((f & 0xFFu) << 8)) : f;
   const uint32_t fo = l4_field(rx.proto);
@@ -1502,10 +1504,11 @@ __device__ __forceinline__ void put_be16(uint8_t *q, uint32_t r) {
 // total lengths through hl/tl.
 __device__ __forceinline__ void rx_parse(SegRx &rx, uint32_t sh, uint64_t len, uint32_t &hl,
                                          uint32_t &tl) {
+  // bytes 4j..4j+3 of the header (v_alignbyte with sh 0 returns h[j] itself)
   uint32_t w[5];
 #pragma unroll
-  for (int j = 0; j < 5; ++j)  // bytes 4j..4j+3 of the header
-    w[j] = sh ? __builtin_amdgcn_alignbyte(rx.h[j + 1], rx.h[j], sh) : rx.h[j];
+  for (int j = 0; j < 5; ++j)
+    if (j != 1) w[j] = __builtin_amdgcn_alignbyte(rx.h[j + 1], rx.h[j], sh);
   hl = (w[0] & 0xFu) * 4u;                                // HeaderLength()
   tl = ((w[0] >> 8) & 0xFF00u) | (w[0] >> 24);            // TotalLength(), BE
   const uint32_t proto = (w[2] >> 8) & 0xFFu;             // Protocol()
@@ -1513,10 +1516,14 @@ __device__ __forceinline__ void rx_parse(SegRx &rx, uint32_t sh, uint64_t len, u
   // The usual 20-byte header is wholly in registers: its sum in the order of
   // the stream's LE prefix sums (byte 0 is a low byte when the packet starts
   // at an even address), so k_seg needs no point at the header end.
-  uint32_t hs = 0;
+  // Summed straight from the address-aligned window dwords, whose 16-bit halves
+  // already weigh each byte by its address parity: dword 0 less the sh bytes
+  // before the start, dword 5 only those sh bytes' counterparts past byte 20.
+  const uint32_t head = (1u << (8u * sh)) - 1u;
+  uint32_t hs = sad(rx.h[0] & ~head, 0u);
 #pragma unroll
-  for (int j = 0; j < 5; ++j) hs = (sh & 1u) ? sadperm(w[j], kSelSwap, hs) : sad(w[j], hs);
-  rx.hsum = hs;
+  for (int j = 1; j < 5; ++j) hs = sad(rx.h[j], hs);
+  rx.hsum = sad(rx.h[5] & head, hs);
   rx.h20 = valid && hl == 20u;
   const bool l4 = valid && (proto == 6u || proto == 17u || proto == 1u);
   rx.flags = valid ? 0u : YU_RX_INVALID;
@@ -1591,6 +1598,9 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   // (uniform batches with sparser strides take k_loop_rx, pick_uniform). Half the
   // VALU work on every point test and offset.
   using Pos = typename std::conditional<K == kSegPlain, uint64_t, uint32_t>::type;
+  // CH < 64: lane CH holds no packet but sits at the chunk's end, so its start
+  // point is the chunk's end point and every packet's end is its successor's start
+  constexpr bool kMarker = CH < 64;
   constexpr Pos kNoPt = ~(Pos)0;             // a point slot not in use
 
   uint64_t ch = wave;
@@ -1618,7 +1628,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
     pt[0].x = x;
     // ragged packets lie back to back: P(end) is the next lane's P(start), so
     // only lane 63 evaluates an end point (the chunk end); RX needs none
-    pt[1].x = RX || (contig && lane != 63u) ? kNoPt : y;
+    pt[1].x = RX || (contig && (kMarker || lane != 63u)) ? kNoPt : y;
     if (tx) {  // the checksum field, when the packet holds it
       const bool f = fld + 2u <= len;
       fx = f ? x + fld : kNoPt;
@@ -1628,11 +1638,10 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
     if (RX) {  // header and transport ends, once the header is parsed
       const uint32_t sh = (uint32_t)x & 3u;
       rx.need = len >= 20u ? (1u << (((19u + sh) >> 2) + 1u)) - 1u : 0u;
+      // an unparsed packet (len < 20) reports only these; rx_parse sets the rest
       rx.flags = YU_RX_INVALID;
-      rx.pseudo = rx.proto = 0u;
-      rx.ipf = rx.hl = rx.fo = rx.h20 = rx.hsum = 0u;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
+      rx.hl = rx.fo = rx.tnext = 0u;
+      pt[2].x = pt[3].x = kNoPt;
       if (DG) {
         pt[2].x = pt[3].x = fx = kNoPt;
         fk = fsum = 0u;
@@ -1685,7 +1694,8 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
     }
     bool here = false;
 #pragma unroll
-    for (int i = 0; i < NP; ++i) here |= pt[i].x - tb < T;
+    for (int i = 0; i < NP; ++i)
+      if (!(RX && i == 1)) here |= pt[i].x - tb < T;  // (RX and DG have no end point)
     if (FB) here |= fx - tb < T;
     if (RX) {  // a header window [floor4(start), +24) still being gathered
       const Pos hs = pt[0].x & ~(Pos)3;
@@ -1721,13 +1731,18 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
         if (rx.need == 0u) {
           uint32_t hl, tl;
           rx_parse(rx, (uint32_t)pt[0].x & 3u, cur.oy - cur.ox, hl, tl);
+          // a well-formed datagram fills its packet: in a ragged chunk its
+          // transport end is the next lane's start (the marker lane's, for the
+          // chunk's last packet), already evaluated; when every lane's is, the
+          // wave skips the transport-end slot altogether
+          rx.tnext = contig && kMarker && tl == (uint32_t)(cur.oy - cur.ox) ? 1u : 0u;
           if (DG) {
             // in contract HeaderLength() >= 20: every point lies at or past
             // byte 20, so never in a tile that has gone by
             const uint32_t fo = dg_parse(rx, (uint32_t)pt[0].x & 3u, hl, tl);
             if (rx.hl) {
               pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
-              pt[3].x = pt[0].x + tl;
+              pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
             }
             if (fo) {
               fx = pt[0].x + fo;
@@ -1735,7 +1750,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
             }
           } else {
             pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
-            pt[3].x = pt[0].x + tl;
+            pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
           }
           parsed = true;
         }
@@ -1743,7 +1758,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const Pos q = pt[i].x - tb;
-        if (q < T) {
+        if (!(RX && i == 1) && q < T) {
           const uint32_t k = (uint32_t)q >> 4;
           pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
         }
@@ -1800,7 +1815,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
     }
 #pragma unroll
     for (int i = 0; i < NP; ++i)
-      if (pt[i].x - tb == T) pt[i].p = carry_l;
+      if (!(RX && i == 1) && pt[i].x - tb == T) pt[i].p = carry_l;
     if (exact) {
 #pragma unroll
       for (int i = 0; i < NP; ++i)
@@ -1815,7 +1830,8 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
     const int nl = (int)(lane < 63u ? lane + 1u : 63u);
     const uint32_t nx_p = (uint32_t)__shfl((int)pt[0].p, nl, 64);
     const uint32_t nx_t = (uint32_t)__shfl((int)pt[0].t, nl, 64);
-    const bool own_end = !contig || lane == 63u;
+    const bool own_end = !contig || (!kMarker && lane == 63u);
+    const uint32_t p3 = RX && rx.tnext ? nx_p : pt[3].p;  // P(transport end)
     const uint32_t pe = own_end ? pt[1].p : nx_p;
     const uint32_t te = own_end ? pt[1].t : nx_t;
     const uint64_t p = ch * CH + lane;
@@ -1830,7 +1846,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
         uint32_t ip = 0u, l4 = 0u;
         const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
         if (rx.hl) ip = ~fold32(le_to_be(p2 - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
-        if (rx.fo) l4 = ~fold32(le_to_be(pt[3].p - p2 - fsum, odd) + rx.pseudo) & 0xFFFFu;
+        if (rx.fo) l4 = ~fold32(le_to_be(p3 - p2 - fsum, odd) + rx.pseudo) & 0xFFFFu;
         if (A.out) {  // out[2p], out[2p + 1]: one 32-bit store when aligned
           if (((uintptr_t)A.out & 3u) == 0u) {
             ((uint32_t *)A.out)[p] = ip | (l4 << 16);
@@ -1852,7 +1868,7 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
           const uint32_t ip = fold32(le_to_be(p2 - pt[0].p, odd));
           if (ip == 0u || ip == 0xFFFFu) r |= YU_RX_IP_OK;
           if (r & YU_RX_L4) {
-            const uint32_t l4 = fold32(le_to_be(pt[3].p - p2, odd) + rx.pseudo);
+            const uint32_t l4 = fold32(le_to_be(p3 - p2, odd) + rx.pseudo);
             if (l4 == 0u || l4 == 0xFFFFu) r |= YU_RX_L4_OK;
           }
         }
@@ -2066,8 +2082,12 @@ const Variant kRag = {"k_rag<16,6>", 1536, {k_rag<16, 6, 0>, k_rag<16, 6, 1>, k_
 // plain loads by default: for scattered 32-byte header reads they beat nt
 // ones (30.7 vs 32.5 us, kbench 12)
 const Variant kHdr = {"k_hdr", 0, {k_hdr<0>, k_hdr<1>, k_hdr<0>}, 64, 64};
+// 64 packets per chunk. (63 packets and a marker lane, kMarker, which drops the
+// end-point slot: small RX datagrams 27.0 -> 26.6 us, but config 4 703 -> 714 and
+// U{64..1500} 127 -> 129 from the 1.6 % more chunks; the 16-packet chunks use it.
+// profiles/r03/kbench_ab_kseg_lean.log)
 #define YU_SEG(U, K, name) \
-  {name, 0, {k_seg<U, 0, K>, k_seg<U, 1, K>, k_seg<U, 1, K>}, 64, 64}
+  {name, 0, {k_seg<U, 0, K, 64>, k_seg<U, 1, K, 64>, k_seg<U, 1, K, 64>}, 64, 64}
 #define YU_SEG16(U, K, name) \
   {name, 0, {k_seg<U, 0, K, 16>, k_seg<U, 1, K, 16>, k_seg<U, 1, K, 16>}, 64, 16}
 const Variant kSeg4 = YU_SEG(4, kSegPlain, "k_seg<4>");
