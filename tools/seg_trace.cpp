@@ -72,15 +72,17 @@ int main(int argc, char **argv) {
   printf("n %lu  U{40..%d}  mode %d  rc %d  traced launch %.1f us  kernel %s\n", (unsigned long)n, hi, mode, rc,
          ms * 1e3, yu_ragged_variant_n(mode, n));
   // segments between the 7 stamps of a step (ticks = shader clock cycles)
-  const char *seg[6] = {"geom+offs", "tile issue+wait c0", "wait rest", "scans", "park/points", "epilogue"};
+  // kind 0/1 (scan path: mid / last step): ... scans, park/points, epilogue;
+  // kind 2 (one-tile chunk summed per lane): ... park, range sums, parse + results
+  const char *seg[6] = {"geom+offs", "tile issue+wait c0", "wait rest", "scans|park", "points|sums", "epilogue|parse"};
   struct Acc { double s[6] = {0, 0, 0, 0, 0, 0}; double tot = 0; int cnt = 0; };
-  Acc last_a, mid_a;
+  Acc last_a, mid_a, ls_a;
   std::vector<double> starts, ends;
   for (uint64_t w = 0; w < nsamp; ++w) {
     for (int k = 0; k < 64; ++k) {
       const uint64_t *q = &h[(w * 64 + k) * 8];
       if (!q[0]) break;
-      Acc &a = (q[7] & 0xFF) ? last_a : mid_a;
+      Acc &a = (q[7] & 0xFF) == 2 ? ls_a : ((q[7] & 0xFF) ? last_a : mid_a);
       for (int j = 0; j < 6; ++j) a.s[j] += (double)(int64_t)(q[j + 1] - q[j]);
       a.tot += (double)(int64_t)(q[6] - q[0]);
       a.cnt++;
@@ -96,6 +98,7 @@ int main(int argc, char **argv) {
   };
   pr("last steps", last_a);
   pr("mid steps", mid_a);
+  pr("lane chunks", ls_a);
   std::sort(starts.begin(), starts.end());
   std::sort(ends.begin(), ends.end());
   if (!starts.empty()) {
