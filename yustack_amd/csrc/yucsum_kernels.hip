@@ -1373,7 +1373,7 @@ struct SegChunk {
 // A chunk is CH packets, lane l < CH owning packet p0 + l; lanes past the
 // chunk (l >= CH) or the batch sit at the chunk's end, so lane 63 always
 // holds it.
-template <int CH>
+template <int CH, bool SIDE = true>
 __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
                                          uint64_t p0, uint32_t lane, SegChunk &k) {
   const uint64_t n = A.n;
@@ -1389,7 +1389,7 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
   const uint64_t rx = offs[A.offsets ? (own ? i : ce) : 0];
   k.ox = A.offsets ? rx : (own ? i * A.stride : uy);
   k.oy = A.offsets ? ry : uy;
-  k.sd = load_side(sp, own ? i : n - 1);  // b0/xe: seg_geom
+  if (SIDE) k.sd = load_side(sp, own ? i : n - 1);  // b0/xe: seg_geom
 }
 
 
@@ -1441,6 +1441,21 @@ __device__ __forceinline__ uint32_t seg_part(const uint4 &d, uint32_t r) {
     acc = BYTES ? __builtin_amdgcn_sad_u8(x, 0u, acc) : sad(x, acc);
   }
   return acc;
+}
+
+// P (or T, BYTES) at tile offset q from the parked tile: the exclusive prefix at
+// q's 8-byte half chunk (pre2: two per 16-byte chunk, at its start and middle)
+// plus the bytes of that half chunk before q. One 4-byte and one 8-byte LDS read
+// and ~10 VALU (a 16-byte chunk prefix needed the 16 bytes and twice the VALU).
+template <bool BYTES>
+__device__ __forceinline__ uint32_t seg_point(const uint32_t *pre2, const uint2 *half, uint32_t q) {
+  const uint32_t h = q >> 3, r = q & 7u;
+  const uint2 d = half[h];
+  const uint32_t mk = (1u << (8u * (r & 3u))) - 1u;
+  const uint32_t lo = r >= 4u ? d.x : (d.x & mk);
+  const uint32_t hi = r >= 4u ? (d.y & mk) : 0u;
+  return BYTES ? __builtin_amdgcn_sad_u8(hi, 0u, __builtin_amdgcn_sad_u8(lo, 0u, pre2[h]))
+               : sad(hi, sad(lo, pre2[h]));
 }
 
 // One point of a lane: position x (relative to b0), and P / T at x once the
@@ -1580,7 +1595,9 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   constexpr uint32_t T = 64u * 16u * U;
   constexpr uint32_t NC = 64u * U;  // chunks per tile
   __shared__ uint4 s_data[4][NC];   // the tile's bytes
-  __shared__ uint32_t s_pre[4][NC];  // chunk-exclusive prefixes (L, then T)
+  // exclusive prefixes per 16-byte chunk (plain kind: L, then T) or per 8-byte half
+  // chunk (the others, seg_point)
+  __shared__ uint32_t s_pre[4][K == kSegPlain ? NC : 2 * NC];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t wave = grid_wave(A.xcd);
@@ -1601,13 +1618,16 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   // CH < 64: lane CH holds no packet but sits at the chunk's end, so its start
   // point is the chunk's end point and every packet's end is its successor's start
   constexpr bool kMarker = CH < 64;
+  // points from half-chunk prefixes (seg_point): the 32-bit kinds; the plain
+  // kind's registers (exact path) leave no room for the halves' sums
+  constexpr bool HP = K != kSegPlain;
   constexpr Pos kNoPt = ~(Pos)0;             // a point slot not in use
 
   uint64_t ch = wave;
   if (wave >= nwave || ch * CH >= A.n) return;
   SegChunk cur, nxt;
-  seg_load<CH>(A, sp, ch * CH, lane, cur);
-  seg_load<CH>(A, sp, (ch + nwave) * CH, lane, nxt);
+  seg_load<CH, !RX>(A, sp, ch * CH, lane, cur);
+  seg_load<CH, !RX>(A, sp, (ch + nwave) * CH, lane, nxt);
   seg_geom(data, A.n, ch * CH, cur);
 
   // per-chunk state
@@ -1665,17 +1685,19 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
                   // step's tile loads, so waiting on them never waits on those
     if (last) {
       seg_geom(data, A.n, (ch + nwave) * CH, nxt);
-      seg_load<CH>(A, sp, (ch + 2u * nwave) * CH, lane, nn);
+      seg_load<CH, !RX>(A, sp, (ch + 2u * nwave) * CH, lane, nn);  // (RX, DG: no side data)
     }
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
                           end, cn);
 
     // chunk sums, address-ordered exclusive prefixes (DPP scan per u)
     const Pos tb = (Pos)(t * T);
-    uint32_t pl[U], ptt[U];
+    // chunk prefix; HP: also the chunk's first half's sum (half-chunk prefixes)
+    uint32_t pl[U], ph[U], ptt[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t s = sum_full<false>(c[u], 0u, 0u);
+      ph[u] = sad(c[u].y, sad(c[u].x, 0u));
+      const uint32_t s = sad(c[u].w, sad(c[u].z, ph[u]));
       const uint32_t inc = group_total<64>(s);
       pl[u] = carry_l + inc - s;
       carry_l += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
@@ -1705,7 +1727,10 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         s_data[wid][u * 64 + lane] = c[u];
-        s_pre[wid][u * 64 + lane] = pl[u];
+        if (HP)
+          ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl[u], pl[u] + ph[u]);
+        else
+          s_pre[wid][u * 64 + lane] = pl[u];
       }
       __builtin_amdgcn_wave_barrier();
       bool parsed = false;
@@ -1759,8 +1784,12 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
       for (int i = 0; i < NP; ++i) {
         const Pos q = pt[i].x - tb;
         if (!(RX && i == 1) && q < T) {
-          const uint32_t k = (uint32_t)q >> 4;
-          pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
+          if (HP) {
+            pt[i].p = seg_point<false>(s_pre[wid], (const uint2 *)s_data[wid], (uint32_t)q);
+          } else {
+            const uint32_t k = (uint32_t)q >> 4;
+            pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
+          }
         }
       }
       if (FB) {  // the field's bytes, weighted by address parity
