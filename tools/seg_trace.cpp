@@ -1,9 +1,9 @@
 // seg_trace.cpp — measurement tool (not product): per-step timeline of k_seg on a
 // small-packet ragged batch (kbench config 16: 1M U{40..200} VERIFY_RX datagrams),
-// from s_memtime stamps the DEBUG side build (tools/old, round 3) records for every
-// 61st wave: step start, after the next chunk's geometry/offset loads, after the
-// next tile's loads are issued (and the current tile's first chunk has landed), after
-// its last chunk has landed, end of step.
+// from s_memtime stamps the DEBUG side build records for every 61st wave: step start,
+// after the next chunk's geometry/offset loads, after the next tile's loads are issued
+// (and the current tile's first chunk has landed), after its last chunk has landed,
+// end of step. Side build: tools/side_build.sh tools/old HEAD tools/seg_trace_patch.py
 // build: hipcc -O2 --offload-arch=gfx950 -I include tools/seg_trace.cpp -o tools/seg_trace -L tools/old -lyucsum -Wl,-rpath,'$ORIGIN/old'
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -77,6 +77,7 @@ int main(int argc, char **argv) {
   const char *seg[6] = {"geom+offs", "tile issue+wait c0", "wait rest", "scans|park", "points|sums", "epilogue|parse"};
   struct Acc { double s[6] = {0, 0, 0, 0, 0, 0}; double tot = 0; int cnt = 0; };
   Acc last_a, mid_a, ls_a;
+  double gaps[2] = {0, 0}; int ngaps[2] = {0, 0};
   std::vector<double> starts, ends;
   for (uint64_t w = 0; w < nsamp; ++w) {
     for (int k = 0; k < 64; ++k) {
@@ -86,6 +87,11 @@ int main(int argc, char **argv) {
       for (int j = 0; j < 6; ++j) a.s[j] += (double)(int64_t)(q[j + 1] - q[j]);
       a.tot += (double)(int64_t)(q[6] - q[0]);
       a.cnt++;
+      if (k > 0) {  // gap from the previous step's last stamp to this step's first
+        const uint64_t *pq = &h[(w * 64 + k - 1) * 8];
+        gaps[(pq[7] & 0xFF) ? 1 : 0] += (double)(int64_t)(q[0] - pq[6]);
+        ngaps[(pq[7] & 0xFF) ? 1 : 0]++;
+      }
       if (k == 0) starts.push_back((double)q[0]);
       if (k == 63 || !h[(w * 64 + k + 1) * 8]) ends.push_back((double)q[6]);
     }
@@ -99,6 +105,8 @@ int main(int argc, char **argv) {
   pr("last steps", last_a);
   pr("mid steps", mid_a);
   pr("lane chunks", ls_a);
+  printf("gap to the next step's start: after a mid step %.0f ticks (n=%d), after a chunk's last step %.0f (n=%d)\n",
+         ngaps[0] ? gaps[0] / ngaps[0] : 0.0, ngaps[0], ngaps[1] ? gaps[1] / ngaps[1] : 0.0, ngaps[1]);
   std::sort(starts.begin(), starts.end());
   std::sort(ends.begin(), ends.end());
   if (!starts.empty()) {
