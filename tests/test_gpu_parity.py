@@ -4,12 +4,18 @@ Small cases cover every mode × layout × alignment × edge length; the full BAS
 configs (2, 3, 4) are compared packet-for-packet against the multithreaded C oracle
 on the same bytes.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
 from oracle import oracle as O
 from yustack_amd import batch
+
+# a measurement run that forces the ragged kernel (YU_RAGGED) checks parity only:
+# the default ragged kernel choice is not asserted then
+FORCED = bool(os.environ.get("YU_RAGGED"))
 
 pytestmark = pytest.mark.gpu
 
@@ -140,7 +146,7 @@ def test_ragged_all_modes(dev, oracle_c, mode, npk):
     lo = {O.MODE_UDP: 8, O.MODE_TCP: 60, O.MODE_VERIFY_TCP: 60, O.MODE_ICMP: 4,
           O.MODE_IPV4: 60, O.MODE_VERIFY_IPV4: 60}.get(mode, 0)
     if mode not in (O.MODE_IPV4, O.MODE_VERIFY_IPV4):
-        assert batch.ragged_variant(mode, npk).startswith("k_loop" if npk <= 4096 else "k_seg")
+        assert FORCED or batch.ragged_variant(mode, npk).startswith("k_loop" if npk <= 4096 else "k_seg")
     lens = rng.integers(lo, 9001, size=npk)
     lens[:len(EDGE_LENS)] = np.maximum(np.array(EDGE_LENS), lo)
     blob, offs = _ragged(rng, lens, base_off=3)
@@ -224,7 +230,7 @@ def test_verify_rx_ragged(dev, oracle_c, lo, hi, npk):
     """Whole received datagrams (tun RX bursts): header + transport verification
     bits against the oracle, every start alignment, valid and damaged packets."""
     import rxgen
-    assert batch.ragged_variant("verify_rx", npk) == ("k_loop<4,rx>" if npk <= 4096 else "k_seg<8,rx,c16>")
+    assert FORCED or batch.ragged_variant("verify_rx", npk) == ("k_loop<4,rx>" if npk <= 4096 else "k_seg<8,rx,c16>")
     rng = np.random.default_rng(9100 + hi + npk)
     blob, offs = rxgen.rx_batch(rng, npk, lo=lo, hi=min(hi, 65535 - 80))
     for base_off in (0, 1, 2, 3):
@@ -411,7 +417,7 @@ def test_tx_datagram_header_straddles_tile(dev, oracle_c, npk, kern):
     datagrams start with floor4(start) 4..20 bytes before a 4 KiB and an 8 KiB tile
     boundary of their chunk (rxgen.tile_edge_batch), at every start alignment."""
     import rxgen
-    assert batch.ragged_variant("tx_datagram", npk) == kern
+    assert FORCED or batch.ragged_variant("tx_datagram", npk) == kern
     chunk = 16 if "c16" in kern else 64
     rng = np.random.default_rng(9600 + npk)
     special = lambda r, total: rxgen.tx_packet(r, max(0, total - 20), ihl=5)  # noqa: E731
@@ -505,7 +511,7 @@ def test_verify_rx_header_straddles_tile(dev, oracle_c, npk, kern):
     uniform slots of 8188 / 4092 bytes (packet k of a chunk then sits 4k bytes before
     the k-th 8 / 4 KiB boundary)."""
     import rxgen
-    assert batch.ragged_variant("verify_rx", npk) == kern
+    assert FORCED or batch.ragged_variant("verify_rx", npk) == kern
     chunk = 16 if "c16" in kern else 64
     rng = np.random.default_rng(9300 + npk)
     for base_off in (0, 1, 2, 3):
@@ -1338,8 +1344,8 @@ def test_ragged_batch_size_cutovers(dev, oracle_c, mode):
     import rxgen
     for npk, want in ((4096, "k_loop"), (4097, "c16"), (65535, "c16"), (65536, "k_seg")):
         name = batch.ragged_variant(mode, npk)
-        assert name.startswith(want) or want in name, (npk, name)
-        if npk == 65536:
+        assert FORCED or name.startswith(want) or want in name, (npk, name)
+        if npk == 65536 and not FORCED:
             assert "c16" not in name
         rng = np.random.default_rng(npk + mode)
         if mode == O.MODE_VERIFY_RX:
