@@ -873,6 +873,31 @@ def test_full_config4_ragged(dev, oracle_c):
     assert np.array_equal(got, want)
 
 
+# ------------------------------------------------------------------ kernel-verified datagrams
+def test_kernel_verified_datagrams_on_gpu(dev):
+    """Datagrams whose checksums the Linux kernel verified over a tun link, and datagrams
+    the kernel built itself (tests/golden/kernel_verified.npz,
+    tests/golden/make_kernel_verified.py): the HIP TX_DATAGRAM path gives exactly the
+    fields the kernel accepted, in place it restores every byte of them, and the HIP
+    VERIFY_RX path passes the kernel's own checksums; at aligned and odd starts."""
+    from test_kernel_verified import RX_OK, load, stored_fields
+    sb, so, kb, ko = load()
+    z, want = stored_fields(sb, so)
+    for base in (0, 1, 3):
+        pad = lambda b: np.concatenate([np.zeros(base, np.uint8), b, np.zeros(16, np.uint8)])  # noqa: E731
+        got = batch.checksum_ragged(_to(dev, pad(z)), _to(dev, (so + base).view(np.int64)),
+                                    "tx_datagram").cpu().numpy()
+        assert np.array_equal(got, want), (base, np.nonzero(got != want)[0][:10])
+        for blob, offs in ((kb, ko), (sb, so)):
+            rx = batch.checksum_ragged(_to(dev, pad(blob)), _to(dev, (offs + base).view(np.int64)),
+                                       "verify_rx").cpu().numpy()
+            assert np.all(rx & RX_OK == RX_OK), (base, rx)
+    d = _to(dev, np.concatenate([z, np.zeros(16, np.uint8)]))
+    got = batch.checksum_ragged(d, _to(dev, so.view(np.int64)), "tx_datagram", fill=True).cpu().numpy()
+    assert np.array_equal(got, want)
+    assert np.array_equal(d.cpu().numpy()[:sb.size], sb)
+
+
 # ------------------------------------------------------------------ reference-executed vectors
 def test_refexec_vectors_on_gpu(dev):
     """The HIP path against known answers produced by executing the reference's own Go

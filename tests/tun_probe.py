@@ -71,6 +71,9 @@ class Probe:
         self.stack, self.host = socket.inet_aton(STACK_ADDR), socket.inet_aton(HOST_ADDR)
         self.route = Route(LocalAddress=self.stack, RemoteAddress=self.host)
         self.sent = self.oracle_mismatch = self.bad_replies = 0
+        # what the fixture generator keeps (tests/golden/make_kernel_verified.py)
+        self.sent_ok: list[bytes] = []      # undamaged datagrams written to the kernel
+        self.from_kernel: list[bytes] = []  # datagrams the kernel wrote back
 
     def close(self) -> None:
         os.close(self.fd)
@@ -79,6 +82,7 @@ class Probe:
         if corrupt_at is None:
             if stored_fields(dgram) != oracle_fields(dgram):
                 self.oracle_mismatch += 1
+            self.sent_ok.append(bytes(dgram))
         else:
             dgram[corrupt_at] ^= 0x01
         os.write(self.fd, bytes(dgram))
@@ -94,6 +98,7 @@ class Probe:
             if len(pkt) >= 20 and pkt[0] >> 4 == 4 and pkt[16:20] == self.stack and want(pkt):
                 if oracle_rx(pkt) & RX_OK != RX_OK:
                     self.bad_replies += 1
+                self.from_kernel.append(pkt)
                 return pkt
         return None
 
@@ -107,6 +112,22 @@ class Probe:
         self._send(packets.send_icmpv4(self.route, 8, 0, data), corrupt_at)
         rep = self._recv(lambda p: p[9] == 1 and p[20] == 0 and p[24:28] == data[:4], timeout)
         return rep is not None and rep[28:struct.unpack_from(">H", rep, 2)[0]] == payload
+
+    # UDP ---------------------------------------------------------------
+    def kernel_udp(self, payloads: list[bytes], port: int = 12345, timeout: float = 0.5) -> int:
+        """Datagrams a kernel UDP socket sends to the stack side (their checksums are
+        the kernel's); returns how many came through the tun."""
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        try:
+            s.bind((HOST_ADDR, 0))
+            got = 0
+            for data in payloads:
+                s.sendto(data, (STACK_ADDR, port))
+                if self._recv(lambda p: p[9] == 17 and p[28:] == data, timeout) is not None:
+                    got += 1
+            return got
+        finally:
+            s.close()
 
     # TCP ---------------------------------------------------------------
     def tcp_session(self, port: int, payloads: list[bytes], corrupt_syn: bool = False,
