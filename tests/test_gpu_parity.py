@@ -896,6 +896,12 @@ def test_kernel_verified_datagrams_on_gpu(dev):
     got = batch.checksum_ragged(d, _to(dev, so.view(np.int64)), "tx_datagram", fill=True).cpu().numpy()
     assert np.array_equal(got, want)
     assert np.array_equal(d.cpu().numpy()[:sb.size], sb)
+    # every other batch mode on the same datagrams' segments and headers
+    from test_kernel_verified import mode_cases
+    for mode, blob, offs, addrs, check in mode_cases():
+        got = batch.checksum_ragged(_to(dev, blob), _to(dev, offs.view(np.int64)), mode,
+                                    addrs=None if addrs is None else _to(dev, addrs)).cpu().numpy()
+        assert check(got), (mode, got)
 
 
 # ------------------------------------------------------------------ reference-executed vectors

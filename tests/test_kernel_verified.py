@@ -50,3 +50,58 @@ def test_oracle_verify_rx_passes_kernel_datagrams():
     for blob, offs in ((kb, ko), (sb, so)):
         got = O.C().batch(blob, O.MODE_VERIFY_RX, offsets=offs)
         assert np.all(got & RX_OK == RX_OK), got
+
+
+def mode_cases():
+    """Every batch mode on the fixture's datagrams, pooled from both sets: (mode,
+    ragged blob, offsets, {src,dst} records or None, check). The transport modes take
+    each datagram's segment (TCP / UDP / ICMP) and its addresses, the IPv4 modes its
+    header. The TX modes see the field zeroed (Encode leaves it 0) and must give the
+    stored value; the VERIFY modes see it as sent and must sum to 0 or 0xFFFF
+    (checker/checker.go:32-35,80-92)."""
+    sb, so, kb, ko = load()
+    dg = [b[s:e] for b, o in ((sb, so), (kb, ko)) for s, e in zip(o[:-1].astype(np.int64), o[1:].astype(np.int64))]
+
+    def pack(parts):
+        offs = np.zeros(len(parts) + 1, np.uint64)
+        offs[1:] = np.cumsum([len(x) for x in parts])
+        return np.concatenate(parts + [np.zeros(16, np.uint8)]), offs
+
+    cases = []
+    for proto, tx, verify, fo in ((6, O.MODE_TCP, O.MODE_VERIFY_TCP, 16), (17, O.MODE_UDP, O.MODE_VERIFY_UDP, 6),
+                                  (1, O.MODE_ICMP, None, 2)):
+        segs, zsegs, addrs, fields = [], [], [], []
+        for d in dg:
+            if int(d[9]) != proto:
+                continue
+            hl, tl = int(d[0] & 0xF) * 4, int(d[2]) << 8 | int(d[3])
+            seg = d[hl:tl].copy()
+            fields.append(int(seg[fo]) << 8 | int(seg[fo + 1]))
+            segs.append(seg.copy())
+            seg[fo:fo + 2] = 0
+            zsegs.append(seg)
+            addrs.append(d[12:20])
+        want = np.array(fields, np.uint16)
+        ad = np.concatenate(addrs) if proto != 1 else None
+        cases.append((tx, *pack(zsegs), ad, lambda got, want=want: np.array_equal(got, want)))
+        if verify is not None:
+            cases.append((verify, *pack(segs), ad, lambda got: np.all((got == 0) | (got == 0xFFFF))))
+    hdrs, zhdrs, fields = [], [], []
+    for d in dg:
+        h = d[:int(d[0] & 0xF) * 4].copy()
+        fields.append(int(h[10]) << 8 | int(h[11]))
+        hdrs.append(h.copy())
+        h[10:12] = 0
+        zhdrs.append(h)
+    want = np.array(fields, np.uint16)
+    cases.append((O.MODE_IPV4, *pack(zhdrs), None, lambda got, want=want: np.array_equal(got, want)))
+    cases.append((O.MODE_VERIFY_IPV4, *pack(hdrs), None, lambda got: np.all((got == 0) | (got == 0xFFFF))))
+    return cases
+
+
+def test_oracle_every_mode_on_kernel_datagrams():
+    cases = mode_cases()
+    assert {c[0] for c in cases} == {O.MODE_TCP, O.MODE_VERIFY_TCP, O.MODE_UDP, O.MODE_VERIFY_UDP,
+                                     O.MODE_ICMP, O.MODE_IPV4, O.MODE_VERIFY_IPV4}
+    for mode, blob, offs, addrs, check in cases:
+        assert check(O.C().batch(blob, mode, offsets=offs, addrs=addrs)), mode
