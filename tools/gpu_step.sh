@@ -1,15 +1,13 @@
-# k_seg TX/RX/DG: one scan per tile over lane-contiguous sums (TS) vs HEAD (tools/old): parity, then A/B
+# k_seg grid: exactly the resident blocks (YU_BLOCKS_PER_CU=3/4, no idle blocks that exit) vs the default over-sized grid
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_ts.log 2>&1 || { tail -30 gpurun_out/gpu_tests_ts.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_ts.log
-O=LD_LIBRARY_PATH=tools/old
-bash tools/ab.sh "16 $O" "16" "15 $O" "15" "8 $O" "8" "5 KB_MODE=8 $O" "5 KB_MODE=8" "14 KB_LEN=160 $O" "14 KB_LEN=160" "7 $O" "7" "6 $O" "6" \
-  "16 $O" "16" "15 $O" "15" "8 $O" "8" "5 KB_MODE=8 $O" "5 KB_MODE=8" "7 $O" "7" > gpurun_out/kbench_ab_ts.log 2>&1 || { tail gpurun_out/kbench_ab_ts.log; exit 1; }
+B3=YU_BLOCKS_PER_CU=3
+bash tools/ab.sh "16" "16 $B3" "16 YU_BLOCKS_PER_CU=4" "6" "6 $B3" "8" "8 $B3" "5" "5 $B3" "5 KB_MODE=8" "5 KB_MODE=8 $B3" \
+  "4" "4 $B3" "7" "7 $B3" "15" "15 $B3" "16" "16 $B3" "6" "6 $B3" > gpurun_out/kbench_ab_seg_grid.log 2>&1 || { tail gpurun_out/kbench_ab_seg_grid.log; exit 1; }
 python3 - <<'PY'
 import re,statistics,collections
 d=collections.defaultdict(list);cur=None
-for l in open('gpurun_out/kbench_ab_ts.log'):
+for l in open('gpurun_out/kbench_ab_seg_grid.log'):
     if l.startswith('=='): cur=l[3:].strip(); continue
     m=re.search(r'round \d+:\s+([\d.]+) us',l)
     if m and cur: d[cur].append(float(m.group(1)))
