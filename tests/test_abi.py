@@ -197,3 +197,19 @@ def test_variant_selection(stride, length, mode, align, want):
 ])
 def test_variant_selection_by_batch_size(stride, length, n, want):
     assert batch.variant(stride, length, "raw", 0, n=n) == want
+
+
+# k_seg's TX / RX / DG kinds keep positions in 32 bits: 63 strides plus a 65535-byte
+# packet and its 3 head bytes must stay under 2 GiB (kSeg32Stride in yucsum_kernels.hip)
+SEG32_STRIDE = ((1 << 31) - 65535 - 3) // 63
+
+
+@pytest.mark.parametrize("mode,kern,loop", [("verify_rx", "k_seg<8,rx>", "k_loop<4,rx>"),
+                                             ("tx_datagram", "k_seg<8,dg>", "k_loop<4,dg>")])
+def test_sparse_datagram_batches_leave_k_seg(mode, kern, loop):
+    """Uniform VERIFY_RX / TX_DATAGRAM batches whose 64-packet chunk could span 2 GiB
+    take a wave per datagram instead (a GPU run at that size would need > 100 GB)."""
+    n = 1 << 20
+    assert batch.variant(1500, 1500, mode, 0, n=n) == kern
+    assert batch.variant(SEG32_STRIDE, 1500, mode, 0, n=n) == kern
+    assert batch.variant(SEG32_STRIDE + 1, 1500, mode, 0, n=n) == loop
