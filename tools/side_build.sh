@@ -21,5 +21,7 @@ done
 get include/yucsum.h "$D/include/yucsum.h"
 if [ -n "$PATCH" ]; then python3 "$PATCH" "$D/yustack_amd/csrc/yucsum_kernels.hip"; fi
 make -s -C "$D/yustack_amd/csrc" -j8
-cp "$D/yustack_amd/libyucsum.so" "$D/libyucsum.so"
+# one copy of the library, no objects: every gpurun call ships the tree
+mv "$D/yustack_amd/libyucsum.so" "$D/libyucsum.so"
+rm -rf "$D/yustack_amd/csrc/build"
 echo "built $D/libyucsum.so from ${REV}${PATCH:+ + $PATCH}"
