@@ -1190,7 +1190,7 @@ __device__ __forceinline__ void rag_fetch(const BatchArgs &A, const SidePtrs &sp
 // fallback for steps holding a packet longer than the group window.
 template <bool BE>
 __device__ __forceinline__ uint32_t rag_serial_sum(uint64_t sabs, uint32_t len, uint32_t E,
-                                                   int mode, uint32_t lane, uint64_t end,
+                                                   uint32_t lane, uint64_t end,
                                                    uint32_t (&jx)[3], const Junk &j) {
   constexpr uint32_t W = 64u * 16u * 4u;
   const uint32_t sh = (uint32_t)(sabs & 3u);
@@ -1317,8 +1317,8 @@ __global__ __launch_bounds__(256) void k_rag(BatchArgs A) {
       }
       const Junk j = make_junk(sh, E, mode);
       uint32_t pjx[3];
-      const uint32_t v = plen > kLEMax ? rag_serial_sum<true>(pabs, E - sh, E, mode, lane, end, pjx, j)
-                                       : rag_serial_sum<false>(pabs, E - sh, E, mode, lane, end, pjx, j);
+      const uint32_t v = plen > kLEMax ? rag_serial_sum<true>(pabs, E - sh, E, lane, end, pjx, j)
+                                       : rag_serial_sum<false>(pabs, E - sh, E, lane, end, pjx, j);
       const Side sd = load_side(sp, p);
       if (lane == 63) finish_packet(A, p, v, plen, sd, A.fill ? A.fill + ps : nullptr, E - sh);
     }
