@@ -1,8 +1,6 @@
-# the GPU parity suite with each ragged measurement override forced (k_rag, 4 KiB k_seg, 16-packet
-# chunks, a wave per packet): every ragged kernel the selection can be forced onto, bit-exact
+# read probe: k_seg's 8 KiB tile stream, u-major (k_seg's layout) vs lane-major loads
 set -o pipefail
 mkdir -p gpurun_out
-for r in rag seg4 seg16 loop; do
-  YU_RAGGED=$r timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_forced_$r.log 2>&1 || { tail -30 gpurun_out/gpu_tests_forced_$r.log; exit 1; }
-  echo "$r: $(tail -1 gpurun_out/gpu_tests_forced_$r.log)"
-done
+PROBE_TILES=1 timeout -k 10 120 tools/hbm_probe 126000000 17 > gpurun_out/hbm_probe_tiles_126MB.log 2>&1 || { tail gpurun_out/hbm_probe_tiles_126MB.log; exit 1; }
+PROBE_TILES=1 timeout -k 10 120 tools/hbm_probe 1583349760 2 > gpurun_out/hbm_probe_tiles_1.58GB.log 2>&1 || { tail gpurun_out/hbm_probe_tiles_1.58GB.log; exit 1; }
+grep "round 1" gpurun_out/hbm_probe_tiles_126MB.log gpurun_out/hbm_probe_tiles_1.58GB.log

@@ -61,6 +61,45 @@ __global__ __launch_bounds__(256) void read_shift(const uint8_t *__restrict__ p,
   out[tid] = acc;
 }
 
+// k_seg's stream shape: each wave reads 8 KiB tiles (8 dwordx4 per lane), the next
+// tile in flight while the current one is summed. LM = false: load u covers the
+// tile's u-th KiB (lane L takes 16-byte chunk u*64 + L, k_seg's layout); LM = true:
+// lane L takes the 8 consecutive chunks 8L..8L+7 (each load touches 64 lines).
+template <bool LM, bool NT>
+__global__ __launch_bounds__(256) void read_tile(const uint4 *__restrict__ p, uint64_t n16, uint32_t *out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t ntiles = n16 / 512u;
+  uint32_t acc = 0;
+  auto ld = [&](uint64_t t, uint4 (&c)[8]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t i = t * 512u + (LM ? lane * 8u + (uint32_t)u : (uint32_t)u * 64u + lane);
+      if (NT) {
+        const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(p + i));
+        c[u] = make_uint4(v.x, v.y, v.z, v.w);
+      } else {
+        c[u] = p[i];
+      }
+    }
+  };
+  uint64_t t = wave;
+  if (t < ntiles) {
+    uint4 c[8];
+    ld(t, c);
+    for (; t < ntiles; t += nw) {
+      uint4 cn[8];
+      ld(t + nw < ntiles ? t + nw : t, cn);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += c[u].x + c[u].y + c[u].z + c[u].w;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) c[u] = cn[u];
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 __global__ void fill(uint4 *p, uint64_t n16) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -99,7 +138,27 @@ int main(int argc, char **argv) {
       {"read U1", read_sum<1, false>}, {"read U2", read_sum<2, false>},
       {"read U4", read_sum<4, false>}, {"read U8", read_sum<8, false>},
       {"read U4 nt", read_sum<4, true>}, {"read U8 nt", read_sum<8, true>},
+      {"tile8K u-maj", read_tile<false, false>}, {"tile8K lane-maj", read_tile<true, false>},
+      {"tile8K u-maj nt", read_tile<false, true>}, {"tile8K lane-m nt", read_tile<true, true>},
   };
+  if (getenv("PROBE_TILES")) {  // only the tile shapes, on k_seg's working grids
+    for (int r = 0; r < rounds; ++r)
+      for (int i = 6; i < 10; ++i)
+        for (int bpc : {3, 4, 8}) {
+          int grid = cus * bpc;
+          for (int w = 0; w < 3; ++w) ks[i].fn<<<grid, 256>>>(buf[w % nbuf], n16, out);
+          CK(hipEventRecord(e0));
+          for (int k = 0; k < reps; ++k) ks[i].fn<<<grid, 256>>>(buf[k % nbuf], n16, out);
+          CK(hipEventRecord(e1));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          const double sec = ms / 1e3 / reps;
+          printf("round %d %-16s blocks/CU %2d: %7.1f us  %7.1f GB/s\n", r, ks[i].name, bpc, sec * 1e6,
+                 n16 * 16 / sec / 1e9);
+        }
+    return 0;
+  }
   int bpcs[] = {2, 4, 8, 16};
   printf("buffer %.3f GB x %d rotating, %d CUs\n", bytes / 1e9, nbuf, cus);
   for (int r = 0; r < rounds; ++r) {
