@@ -29,6 +29,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -482,32 +483,67 @@ def _free_port() -> int:
     return p
 
 
+# after SIGTERM, a rank that is still alive gets SIGKILL
+STOP_GRACE_S = float(os.environ.get("YU_BENCH_STOP_GRACE", "10"))
+
+
 def spawn_ranks(plan: dict, argv: list) -> int:
     """The --gpus N launcher: N child processes running this script as ranks 0..N-1
     on 127.0.0.1. Nothing in this process has touched a GPU. A rank that fails takes
-    the others down (their exact PIDs); the exit status is the first failure's."""
+    the others down (their exact PIDs: SIGTERM, then SIGKILL after STOP_GRACE_S), and
+    the exit status is the first failure's. A SIGTERM / SIGINT to the launcher itself
+    (a timeout, ^C) stops the ranks the same way before it exits, so no rank is left
+    running on a GPU."""
     port = _free_port()
     procs = []
-    for r in range(plan["world"]):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(plan["world"]),
-                   LOCAL_WORLD_SIZE=str(plan["world"]), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   YU_BENCH_BACKEND=plan["backend"])
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
-    rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            c = p.poll()
-            if c is None:
-                continue
-            live.remove(p)
-            if c != 0 and rc == 0:
-                rc = c if c > 0 else 128 - c
-                log(f"bench: rank pid {p.pid} exited with {c}; stopping the other ranks")
-                for q in live:
+    stop_at = [None]  # when the ranks were told to stop
+
+    def stop_all():
+        if stop_at[0] is None:
+            stop_at[0] = time.monotonic()
+            for q in procs:
+                if q.poll() is None:
                     q.terminate()
-        time.sleep(0.05)
-    return rc
+
+    def on_signal(signum, _frame):
+        log(f"bench: launcher got signal {signum}; stopping the ranks")
+        stop_all()
+        for q in procs:
+            try:
+                q.wait(STOP_GRACE_S)
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
+        sys.exit(128 + signum)
+
+    prev = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        for r in range(plan["world"]):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(plan["world"]),
+                       LOCAL_WORLD_SIZE=str(plan["world"]), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       YU_BENCH_BACKEND=plan["backend"])
+            procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
+            log(f"bench: rank {r} pid {procs[-1].pid}")
+        rc = 0
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    log(f"bench: rank pid {p.pid} exited with {c}; stopping the other ranks")
+                    stop_all()
+            if stop_at[0] is not None and time.monotonic() - stop_at[0] > STOP_GRACE_S:
+                for q in live:
+                    q.kill()
+            time.sleep(0.05)
+        return rc
+    finally:
+        for sig, h in prev.items():
+            signal.signal(sig, h)
 
 
 def launch_check(plan: dict) -> None:
@@ -516,6 +552,14 @@ def launch_check(plan: dict) -> None:
     launcher and for checking a node's launch before the real run."""
     import torch.distributed as dist
     world = plan["world"]
+    # test hooks (tests/test_bench_launch.py): a rank that fails, one that ignores
+    # SIGTERM, and ranks that are slow to start
+    if os.environ.get("YU_BENCH_LAUNCH_FAIL_RANK") == str(plan["rank"]):
+        sys.exit(3)
+    if os.environ.get("YU_BENCH_LAUNCH_DEAF_RANK") == str(plan["rank"]):
+        signal.signal(signal.SIGTERM, signal.SIG_IGN)
+    if os.environ.get("YU_BENCH_LAUNCH_SLEEP"):
+        time.sleep(float(os.environ["YU_BENCH_LAUNCH_SLEEP"]))
     if world > 1:
         dist.init_process_group("gloo", rank=plan["rank"], world_size=world)
     me = {"rank": plan["rank"], "local": plan["local"], "device": plan["device"], "pid": os.getpid(),

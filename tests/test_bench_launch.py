@@ -85,3 +85,55 @@ def test_failing_rank_fails_the_launch():
     r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-extra", "--no-e2e", "--no-cpu-baseline"])
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def _alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    return True
+
+
+def _spawn(args, env):
+    e = dict(os.environ, **env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "YU_BENCH_BACKEND"):
+        e.pop(k, None)
+    return subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=e,
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
+
+def _rank_pids(p, n, timeout=60):
+    """The launcher logs each rank's pid as it starts it."""
+    import select
+    import time
+    pids, end = {}, time.monotonic() + timeout
+    while len(pids) < n and time.monotonic() < end:
+        r, _, _ = select.select([p.stderr], [], [], 1.0)
+        if r:
+            ln = p.stderr.readline()
+            if ln.startswith("bench: rank ") and " pid " in ln:
+                w = ln.split()
+                pids[int(w[2])] = int(w[4])
+    assert len(pids) == n, pids
+    return list(pids.values())
+
+
+def test_signal_to_launcher_stops_its_ranks():
+    import signal
+    p = _spawn(["--gpus", "2", "--launch-check"], {"YU_BENCH_LAUNCH_SLEEP": "120"})
+    pids = _rank_pids(p, 2)
+    assert all(_alive(x) for x in pids)
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(30) == 128 + signal.SIGTERM
+    assert not any(_alive(x) for x in pids)  # stopped and reaped by the launcher
+
+
+def test_rank_ignoring_sigterm_is_killed_after_grace():
+    # rank 1 fails; rank 0 ignores the SIGTERM that follows and must get SIGKILL
+    p = _spawn(["--gpus", "2", "--launch-check"],
+               {"YU_BENCH_LAUNCH_FAIL_RANK": "1", "YU_BENCH_LAUNCH_DEAF_RANK": "0",
+                "YU_BENCH_LAUNCH_SLEEP": "120", "YU_BENCH_STOP_GRACE": "1"})
+    pids = _rank_pids(p, 2)
+    assert p.wait(60) == 3  # the first failure's status
+    assert not any(_alive(x) for x in pids)
