@@ -260,12 +260,14 @@ def cpu_baseline(w: Workload, threads: int, budget_s: float):
         return reps * b_alg / t / GIB, sample_pk, reps, t
     r1, s1, n1, t1 = rate(1, 1 << 15)
     rT, sT, nT, tT = rate(threads, w.n)
+    wall = t1 + tT
     opt = {}
     flags = open("/proc/cpuinfo").read() if os.path.exists("/proc/cpuinfo") else ""
     if " avx2" in flags:  # the -march=x86-64-v3 build needs AVX2
         C = O.C_opt()  # "optimised CPU" (SURVEY.md §8d): same restatement, vectorised
         o1 = rate(1, 1 << 15)
         oT = rate(threads, w.n)
+        wall += o1[3] + oT[3]
         opt = {"optimised_value": round(oT[0], 3), "optimised_value_1core": round(o1[0], 3),
                "optimised_build": "oracle/csum_oracle.c -O3 -march=x86-64-v3 (vectorised)"}
     return parity, {
@@ -275,7 +277,8 @@ def cpu_baseline(w: Workload, threads: int, budget_s: float):
                    f"{nT} pass(es) over the first {sT} packets of the timed batch in {tT:.1f} s; "
                    f"1 thread: {r1:.3f} GiB/s, {n1} pass(es) over {s1} packets in {t1:.1f} s"),
         "value_1core": round(r1, 3),
-        "cpu_work_s": round(t1 + tT * threads, 1),
+        "cpu_work_s": round(t1 + tT * threads, 1),  # CPU-seconds of the port's two timings
+        "timing_wall_s": round(wall, 1),  # wall time of every timed CPU leg (port and vectorised)
         "cpu_model": cpu_model(),
         "host_cpus_visible": os.cpu_count(),
         **opt,
