@@ -2309,6 +2309,15 @@ int use_nt() {
   return v;
 }
 
+// k_small writing the field in place loads plainly unless YU_NT says otherwise: the
+// field's line is then more often still cached when the 2-byte store reaches it
+// (config 9: 320.9 -> 312.2 us, and 326.2 -> 321.2 on a second box; all-nt 330.2; k_lane's 72-byte writer gains nothing,
+// 29.9 vs 30.8; profiles/r03/kbench_ab_fill_nt.log)
+int fill_nt() {
+  static int v = env_int("YU_NT", 0, 2, 0);
+  return v;
+}
+
 // YU_XCD: 1 = XCD-aware block order (grid_wave), 0 (default) = plain blockIdx.
 // Measured (round 1, tools/ab.sh): no gain on any config — these kernels
 // share at most one line between neighbouring blocks, and the Infinity Cache
@@ -2355,7 +2364,7 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   a.xcd = (uint32_t)use_xcd();
   a.small_waves = (uint32_t)cu_count(dev) * 4u * (uint32_t)seg_small_blocks();
   KernelFn k = A.fill && v.fill ? v.fill : v.fn[use_nt()];
-  if (v.run && !runs) k = v.inter[use_nt()];
+  if (v.run && !runs) k = v.inter[A.fill ? fill_nt() : use_nt()];
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
