@@ -2311,8 +2311,8 @@ int use_nt() {
 
 // k_small writing the field in place loads plainly unless YU_NT says otherwise: the
 // field's line is then more often still cached when the 2-byte store reaches it
-// (config 9: 320.9 -> 312.2 us, and 326.2 -> 321.2 on a second box; all-nt 330.2; k_lane's 72-byte writer gains nothing,
-// 29.9 vs 30.8; profiles/r03/kbench_ab_fill_nt.log)
+// (config 9: 320.9 -> 312.2 us on one box, 326.2 -> 321.2 on another; all-nt 330.2;
+// k_lane's 72-byte writer gains nothing, 29.9 vs 30.8; profiles/r03/kbench_ab_fill_nt.log)
 int fill_nt() {
   static int v = env_int("YU_NT", 0, 2, 0);
   return v;
