@@ -66,8 +66,10 @@ class Workload:
         self.initial_arr = None
         self.addrs = None
         # 9 / 10: configs 3 / 8 through the in-place field writer (SetChecksum on
-        # the device): the field is stored, no uint16 array
-        self.fill = cfg in (9, 10)
+        # the device): the field is stored, no uint16 array;
+        # 12 / 13: the ragged in-place writers (a tun TX burst, both fields of whole
+        # datagrams; small UDP datagrams back to back)
+        self.fill = cfg in (9, 10, 12, 13)
         base = {9: 3, 10: 8}.get(cfg, cfg)
         if base == 2:  # 1M x 64-B UDP payloads: A1 over the payload, pseudo-header partial as initial
             self.mode, self.L = batch.RAW, 64
@@ -84,28 +86,44 @@ class Workload:
             nbytes = n * self.L
             self.side = 8 * n  # addrs
             self.name = "config3: 1M x 1500-B TCP segments incl. pseudo-header (sendTCP field value)"
-        elif cfg in (4, 6, 7, 11):
+        elif cfg in (4, 6, 7, 11, 12, 13):
             # 4: ragged 64..9000 B back-to-back, RAW with initial (BASELINE config 4)
             # 6: tun RX burst, 1M whole IPv4 datagrams U{40..1500} B, VERIFY_RX (§8f row 1)
             # 7: the same with small datagrams U{40..200} B (ACKs, DNS, VoIP)
             # 11: tun TX burst, 1M outgoing TCP/IPv4 datagrams U{40..1500} B, both
             #     checksum fields (TX_DATAGRAM, two results per datagram)
-            self.mode = {4: batch.RAW, 11: batch.TX_DATAGRAM}.get(cfg, batch.VERIFY_RX)
+            # 12: config 11 written in place, the burst tundev writes
+            #     (network/ipv4/ipv4.go:94 + transport/tcp/connect.go:583, then
+            #     link/tundev/tundev.go:171-196): lengths rounded up to 4 B (the
+            #     fill contract: 4-aligned offsets)
+            # 13: 1M sendUDP datagrams U{40..200} B back to back, field in place
+            #     (header/udp.go:60-62), 4-aligned like 12
+            self.mode = {4: batch.RAW, 11: batch.TX_DATAGRAM, 12: batch.TX_DATAGRAM,
+                         13: batch.UDP}.get(cfg, batch.VERIFY_RX)
             rng = np.random.default_rng(cfg)
-            hi = {4: 9001, 6: 1501, 7: 201, 11: 1501}[cfg]
-            lens = rng.integers(64 if cfg == 4 else 40, hi, size=n)
+            hi = {4: 9001, 6: 1501, 7: 201, 11: 1501, 12: 1501, 13: 201}[cfg]
+            lo = 64 if cfg == 4 else 40
+            self.shape = f"U{{{lo}..{hi - 1}}}" + (" rounded up to 4" if cfg in (12, 13) else "")
+            lens = rng.integers(lo, hi, size=n)
+            if cfg in (12, 13):
+                lens = (lens + 3) & ~3
             offs = np.zeros(n + 1, dtype=np.int64)
             offs[1:] = np.cumsum(lens)
             nbytes = int(offs[-1])
             self.L = 0
             self.offsets = torch.from_numpy(offs).to(dev)
             self.lens = torch.from_numpy(lens).to(dev)
-            self.side = 8 * (n + 1) + (2 * n if cfg == 4 else 0)
-            self.name = ("config4: ragged 1M packets U{64..9000} B back-to-back (odd offsets)" if cfg == 4 else
-                         f"tun RX: 1M received IPv4 datagrams U{{40..{hi - 1}}} B back-to-back, header + TCP "
-                         "checksum verification (VERIFY_RX)" if cfg != 11 else
-                         "tun TX: 1M outgoing TCP/IPv4 datagrams U{40..1500} B back-to-back, IPv4 header and "
-                         "TCP checksum fields (TX_DATAGRAM, 2 results per datagram)")
+            self.side = 8 * (n + 1) + (2 * n if cfg == 4 else 0) + (8 * n if cfg == 13 else 0)
+            self.name = {
+                4: "config4: ragged 1M packets U{64..9000} B back-to-back (odd offsets)",
+                11: "tun TX: 1M outgoing TCP/IPv4 datagrams U{40..1500} B back-to-back, IPv4 header and "
+                    "TCP checksum fields (TX_DATAGRAM, 2 results per datagram)",
+                12: "tun TX in place: 1M outgoing TCP/IPv4 datagrams U{40..1500} B (4-aligned) back-to-back, "
+                    "both checksum fields stored into each datagram (yu_csum_fill_ragged, TX_DATAGRAM)",
+                13: "ragged UDP in place: 1M sendUDP datagrams U{40..200} B (4-aligned) back-to-back, "
+                    "field stored into each datagram (yu_csum_fill_ragged, UDP + pseudo-header)",
+            }.get(cfg, f"tun RX: 1M received IPv4 datagrams U{{40..{hi - 1}}} B back-to-back, header + TCP "
+                       "checksum verification (VERIFY_RX)")
         else:
             raise SystemExit(f"unknown config {cfg}")
         self.payload = nbytes
@@ -117,36 +135,41 @@ class Workload:
                 v = d.view(n, self.L)
                 v[:, 12] = 0x50
                 v[:, 16:18] = 0
-            if cfg in (6, 7, 11):  # IPv4 header: IHL 5, TotalLength = packet length, protocol TCP
+            if cfg in (6, 7, 11, 12):  # IPv4 header: IHL 5, TotalLength = packet length, protocol TCP
                 s0 = self.offsets[:-1]
                 d[s0] = 0x45
                 d[s0 + 2] = (self.lens >> 8).to(torch.uint8)
                 d[s0 + 3] = (self.lens & 0xFF).to(torch.uint8)
                 d[s0 + 9] = 6
-                if cfg == 11:  # the TCP segment as sendTCP encodes it: DataOffset 5
+                if cfg in (11, 12):  # the TCP segment as sendTCP encodes it: DataOffset 5
                     d[s0 + 32] = 0x50
             self.data.append(d)
         if cfg == 2 or cfg == 4:
             self.initial_arr = torch.randint(0, 65536, (n,), dtype=torch.int32, device=dev,
                                              generator=g).to(torch.uint16)
-        if self.fill:
+        if self.fill and self.offsets is None:
             self.name += "; fused in-place field writer (yu_csum_fill_uniform, no uint16 array)"
-        if base in (3, 8):
+        if base in (3, 8) or cfg == 13:
             self.addrs = torch.randint(0, 256, (8 * n,), dtype=torch.uint8, device=dev, generator=g)
         self.out = torch.empty(n * batch.outputs(self.mode), dtype=torch.uint16, device=dev)
         if self.offsets is not None:  # validate once; the timed launches skip the check
             batch.checksum_ragged(self.data[0], self.offsets, self.mode,
-                                  initial_arr=self.initial_arr, out=self.out)
+                                  initial_arr=self.initial_arr, addrs=self.addrs, out=self.out)
         # algorithmic bytes per launch: payload + side arrays + uint16 out
         self.bytes = self.payload + self.side + 2 * n * batch.outputs(self.mode)
 
     def step(self, k: int) -> None:
         d = self.data[k % self.R]
-        if self.fill:  # the field goes into the packet; no result array
-            rc = batch.lib().yu_csum_fill_uniform(d.data_ptr(), self.L, self.L, self.n, self.mode, None, 0,
-                                                  self.addrs.data_ptr(), None,
-                                                  torch.cuda.current_stream(self.dev).cuda_stream)
-            batch.check(rc, "yu_csum_fill_uniform")
+        if self.fill:  # the fields go into the packets; no result array
+            stream = torch.cuda.current_stream(self.dev).cuda_stream
+            ad = None if self.addrs is None else self.addrs.data_ptr()
+            if self.offsets is None:
+                rc = batch.lib().yu_csum_fill_uniform(d.data_ptr(), self.L, self.L, self.n, self.mode, None, 0,
+                                                      ad, None, stream)
+            else:
+                rc = batch.lib().yu_csum_fill_ragged(d.data_ptr(), self.offsets.data_ptr(), self.n, self.mode,
+                                                     None, 0, ad, None, stream)
+            batch.check(rc, "yu_csum_fill_uniform" if self.offsets is None else "yu_csum_fill_ragged")
         elif self.offsets is None:
             batch.checksum_uniform(d, self.L, self.L, self.n, self.mode, initial_arr=self.initial_arr,
                                    addrs=self.addrs, out=self.out)
@@ -181,6 +204,7 @@ def timed(w: Workload, steps: int, warmup: int, dist: bool):
     return wall, kern
 
 
+SIDE_CONFIGS = (2, 8, 3, 4, 6, 7, 9, 10, 11, 12, 13)  # every workload; all but --config are side lines
 SIDE_LAUNCHES = 50  # launches per side-config graph, fixed whatever --steps says
 SIDE_SETTLE = 2     # untimed replays first: upload, then ~50 launches of load to leave the clock ramp
 SIDE_TIMED = 3      # timed replays; the per-launch figure is their median
@@ -437,11 +461,67 @@ def _imports():
     np, torch, batch = numpy, _torch, _batch
 
 
-def _device_count() -> int:
-    """GPUs visible to this process, without initialising HIP (device_count does not
-    on this image; nothing else is called)."""
-    import torch as _torch
-    return _torch.cuda.device_count()
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+DRI_DIR = "/dev/dri"
+
+
+def _visible_cut(n: int, value) -> int:
+    """Devices left of n after a HIP_VISIBLE_DEVICES-style list: entries are taken in
+    order up to the first that names no device (an index out of range, or junk),
+    as HIP and ROCr apply them; a GPU-<uuid> entry counts as one device. An empty
+    value hides every device."""
+    if value is None:
+        return n
+    k = 0
+    for tok in value.split(","):
+        tok = tok.strip()
+        if tok.startswith("GPU-") and len(tok) > 4:
+            k += 1
+        elif tok.isdigit() and int(tok) < n:
+            k += 1
+        else:
+            break
+    return min(n, k)
+
+
+def _device_count(env=None, nodes: str = KFD_NODES, dri: str = DRI_DIR) -> int:
+    """GPUs this process can use, counted without loading HIP, so that the --gpus N
+    launcher starts its ranks before anything here has touched a GPU: the KFD topology
+    nodes that are GPUs (gfx_target_version != 0) and whose render node this process
+    can open — the enumeration the ROCm runtime does — then cut by
+    ROCR_VISIBLE_DEVICES, HIP_VISIBLE_DEVICES and CUDA_VISIBLE_DEVICES in that order.
+    Opening a render node is a plain DRM file open (no KFD queue, no HIP).
+    tests/test_bench_launch.py checks the parsing on a fake topology;
+    tests/test_gpu_dist.py checks the count against torch.cuda.device_count()."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        names = sorted(os.listdir(nodes), key=lambda s: int(s) if s.isdigit() else -1)
+    except OSError:
+        names = []
+    for name in names:
+        props = {}
+        try:
+            with open(os.path.join(nodes, name, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    props[k] = v.strip()
+        except OSError:
+            continue
+        if props.get("gfx_target_version", "0") in ("0", ""):
+            continue  # a CPU node
+        minor = props.get("drm_render_minor")
+        if minor is None:
+            continue
+        try:
+            fd = os.open(os.path.join(dri, f"renderD{int(minor)}"), os.O_RDWR | os.O_CLOEXEC)
+        except (OSError, ValueError):
+            continue  # not ours (not passed into this container, or no permission)
+        os.close(fd)
+        n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        n = _visible_cut(n, env.get(var))
+    return n
 
 
 def resolve_launch(gpus: int, env: dict, ndev: int) -> dict:
@@ -454,9 +534,11 @@ def resolve_launch(gpus: int, env: dict, ndev: int) -> dict:
       processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set) before anything here
       touches a GPU, and exits with their status.
 
-    Backend: RCCL ("nccl") when every rank has a GPU of its own; gloo when ranks share
-    fewer GPUs (a rehearsal on a smaller box: RCCL refuses two ranks on one device).
-    YU_BENCH_BACKEND overrides. Rank r runs on device LOCAL_RANK % ndev."""
+    Backend: RCCL ("nccl") when every rank of this node has a GPU of its own (ndev >=
+    LOCAL_WORLD_SIZE, the node's rank count; WORLD_SIZE when the launcher sets none);
+    gloo when the node's ranks share fewer GPUs (a rehearsal on a smaller box: RCCL
+    refuses two ranks on one device). YU_BENCH_BACKEND overrides. Rank r runs on
+    device LOCAL_RANK % ndev."""
     if gpus < 1:
         raise SystemExit(f"--gpus must be >= 1 (got {gpus})")
     ws = env.get("WORLD_SIZE")
@@ -467,15 +549,17 @@ def resolve_launch(gpus: int, env: dict, ndev: int) -> dict:
                              "pass --gpus equal to --nproc-per-node")
         role = "rank" if world > 1 else "single"
         rank, local = int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", env.get("RANK", "0")))
+        per_node = int(env.get("LOCAL_WORLD_SIZE", world))
     else:
         world, rank, local = gpus, 0, 0
         role = "spawn" if gpus > 1 else "single"
-    backend = env.get("YU_BENCH_BACKEND") or ("nccl" if ndev >= world else "gloo")
+        per_node = world
+    backend = env.get("YU_BENCH_BACKEND") or ("nccl" if ndev >= per_node else "gloo")
     if backend not in ("nccl", "gloo"):
         raise SystemExit(f"YU_BENCH_BACKEND must be nccl or gloo (got {backend})")
-    shared = ndev < world
+    shared = ndev < per_node
     return {"role": role, "world": world, "rank": rank, "local": local, "backend": backend,
-            "ndev": ndev, "device": local % max(1, ndev), "shared": shared}
+            "ndev": ndev, "device": local % max(1, ndev), "shared": shared, "per_node": per_node}
 
 
 def _free_port() -> int:
@@ -582,7 +666,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 6, 7, 8, 9, 10, 11])
+    ap.add_argument("--config", type=int, default=3, choices=SIDE_CONFIGS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the side-config measurements")
     ap.add_argument("--cpu-budget", type=float, default=6.0, help="wall seconds for the CPU baseline")
@@ -649,7 +733,7 @@ def rank_main(args, plan: dict) -> None:
         "config": {
             "workload": w.name + (f"; config5 shape: {world} x 1M packets, one shard per rank" if dist else ""),
             "packets_per_gpu": w.n,
-            "packet_bytes": w.L if w.L else "U{64..9000}",
+            "packet_bytes": w.L if w.L else w.shape,
             "mode": {0: "raw", 1: "udp", 2: "tcp", 8: "verify_rx", 9: "tx_datagram"}.get(w.mode, str(w.mode)),
             "algorithmic_bytes_per_step_per_gpu": w.bytes,
             "rotating_batches": w.R,
@@ -676,7 +760,7 @@ def rank_main(args, plan: dict) -> None:
 
     if rank == 0 and world == 1 and not args.no_extra:
         extra = {}
-        for c in (2, 8, 3, 4, 6, 7, 9, 10, 11):
+        for c in SIDE_CONFIGS:
             if c == args.config:
                 continue
             wc = Workload(c, dev, seed=77 + c)
@@ -699,9 +783,6 @@ def rank_main(args, plan: dict) -> None:
 
     if rank == 0 and world == 1 and not args.no_e2e:
         res["end_to_end_host_memory"] = end_to_end(w)
-    if rank == 0 and dist and not args.no_e2e and plan["ndev"] >= world:
-        # host memory over all the job's GPUs at once, on rank 0 after the timed region
-        res["end_to_end_host_memory"] = host_multi(w, list(range(world)))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         parity, cb = cpu_baseline(w, host_threads(), args.cpu_budget)
@@ -710,11 +791,18 @@ def rank_main(args, plan: dict) -> None:
     else:
         res["cpu_baseline"] = None
 
-    if rank == 0:
-        print(json.dumps(res), flush=True)
     if dist:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+    if rank == 0 and dist and not args.no_e2e and plan["ndev"] >= world:
+        # Host memory over all the job's GPUs at once (rank 0). Taken after the group
+        # is torn down: a rank waiting in an RCCL barrier meanwhile would keep a
+        # collective kernel spinning on its GPU. The other ranks have left the timed
+        # work and hold no kernels; they exit while this runs.
+        res["end_to_end_host_memory"] = host_multi(w, list(range(world)))
+        res["end_to_end_host_memory"]["measured"] = "rank 0 after destroy_process_group; other ranks idle"
+    if rank == 0:
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

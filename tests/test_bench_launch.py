@@ -52,6 +52,62 @@ def test_backend_override():
     assert bench.resolve_launch(2, {"YU_BENCH_BACKEND": "gloo"}, 8)["backend"] == "gloo"
 
 
+def test_backend_follows_ranks_per_node():
+    # 2 nodes x 8 GPUs under torchrun: each node's 8 ranks have a GPU each -> RCCL
+    env = {"WORLD_SIZE": "16", "RANK": "11", "LOCAL_RANK": "3", "LOCAL_WORLD_SIZE": "8"}
+    p = bench.resolve_launch(16, env, 8)
+    assert (p["backend"], p["shared"], p["device"], p["per_node"]) == ("nccl", False, 3, 8)
+    # the same on 4-GPU nodes: ranks share cards -> gloo rehearsal
+    p = bench.resolve_launch(16, env, 4)
+    assert p["backend"] == "gloo" and p["shared"]
+    # no LOCAL_WORLD_SIZE from the launcher: the world is the node
+    p = bench.resolve_launch(8, {"WORLD_SIZE": "8", "RANK": "0", "LOCAL_RANK": "0"}, 8)
+    assert p["per_node"] == 8 and p["backend"] == "nccl"
+
+
+def _fake_topology(tmp_path, gpus_minor, cpus=1, gfx="90500"):
+    """A KFD topology tree: `cpus` CPU nodes, then one GPU node per render minor in
+    gpus_minor; a render node file exists (and opens) only for minors >= 0."""
+    nodes, dri = tmp_path / "nodes", tmp_path / "dri"
+    nodes.mkdir()
+    dri.mkdir()
+    k = 0
+    for _ in range(cpus):
+        (nodes / str(k)).mkdir()
+        (nodes / str(k) / "properties").write_text("cpu_cores_count 64\ngfx_target_version 0\n")
+        k += 1
+    for m in gpus_minor:
+        (nodes / str(k)).mkdir()
+        minor = abs(m)
+        (nodes / str(k) / "properties").write_text(
+            f"simd_count 1024\ngfx_target_version {gfx}\ndrm_render_minor {minor}\n")
+        if m >= 0:
+            (dri / f"renderD{minor}").write_bytes(b"")
+        k += 1
+    return str(nodes), str(dri)
+
+
+def test_device_count_reads_kfd_topology_without_hip(tmp_path):
+    # 3 GPU nodes, of which the process can open two render nodes (the third is not
+    # passed into this container); CPU nodes never count
+    nodes, dri = _fake_topology(tmp_path, [128, 136, -144], cpus=2)
+    assert bench._device_count({}, nodes, dri) == 2
+    assert bench._device_count({"HIP_VISIBLE_DEVICES": "1"}, nodes, dri) == 1
+    assert bench._device_count({"ROCR_VISIBLE_DEVICES": "0,1", "CUDA_VISIBLE_DEVICES": "0"}, nodes, dri) == 1
+    assert bench._device_count({"HIP_VISIBLE_DEVICES": ""}, nodes, dri) == 0
+    assert bench._device_count({"HIP_VISIBLE_DEVICES": "0,5,1"}, nodes, dri) == 1  # stops at the bad index
+    assert bench._device_count({"ROCR_VISIBLE_DEVICES": "GPU-1234abcd"}, nodes, dri) == 1
+    assert bench._device_count({}, str(tmp_path / "absent"), dri) == 0
+    # the counting loaded nothing (the launcher imports the standard library only)
+    assert bench.torch is None
+
+
+def test_device_count_eight_gpu_node(tmp_path):
+    nodes, dri = _fake_topology(tmp_path, [128 + 8 * i for i in range(8)], cpus=2)
+    assert bench._device_count({}, nodes, dri) == 8
+    assert bench.resolve_launch(8, {}, bench._device_count({}, nodes, dri))["backend"] == "nccl"
+
+
 def _run(args, env=None, timeout=240):
     e = dict(os.environ, **(env or {}))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "YU_BENCH_BACKEND"):
@@ -61,7 +117,7 @@ def _run(args, env=None, timeout=240):
                           capture_output=True, text=True, timeout=timeout)
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_self_launch_starts_n_ranks(n):
     r = _run(["--gpus", str(n), "--launch-check"])
     assert r.returncode == 0, r.stderr[-2000:]
@@ -104,17 +160,26 @@ def _spawn(args, env):
 
 
 def _rank_pids(p, n, timeout=60):
-    """The launcher logs each rank's pid as it starts it."""
+    """The launcher logs each rank's pid as it starts it. Read the raw pipe: a
+    buffered readline after select() can leave a second line in the buffer, which
+    select() then never reports."""
     import select
     import time
-    pids, end = {}, time.monotonic() + timeout
+    fd = p.stderr.fileno()
+    pids, buf, end = {}, b"", time.monotonic() + timeout
     while len(pids) < n and time.monotonic() < end:
-        r, _, _ = select.select([p.stderr], [], [], 1.0)
+        r, _, _ = select.select([fd], [], [], 1.0)
         if r:
-            ln = p.stderr.readline()
-            if ln.startswith("bench: rank ") and " pid " in ln:
-                w = ln.split()
-                pids[int(w[2])] = int(w[4])
+            chunk = os.read(fd, 65536)
+            if not chunk:
+                break
+            buf += chunk
+            *lines, buf = buf.split(b"\n")
+            for ln in lines:
+                ln = ln.decode(errors="replace")
+                if ln.startswith("bench: rank ") and " pid " in ln:
+                    w = ln.split()
+                    pids[int(w[2])] = int(w[4])
     assert len(pids) == n, pids
     return list(pids.values())
 

@@ -1,20 +1,78 @@
 """Static checks of the cgo shim (bindings/go/checksum), which this image cannot
 compile (no Go toolchain): every C function it calls is declared in include/yucsum.h
-and exported by libyucsum.so, every C constant it names is defined there, and its cgo
-preamble compiles as C against the header."""
+and exported by libyucsum.so, every C constant it names is defined there, each cgo
+preamble compiles as C against the header, and each file keeps to its Go toolchain
+floor."""
+import glob
 import os
 import re
 import subprocess
 
+import pytest
+
 from yustack_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GO = os.path.join(ROOT, "bindings", "go", "checksum", "checksum.go")
+GODIR = os.path.join(ROOT, "bindings", "go", "checksum")
 HDR = os.path.join(ROOT, "include", "yucsum.h")
+# file -> the newest Go release it may need. The scalar drop-in and the packed-batch
+# calls must build with the Go the reference's unchanged callers need (1.10:
+# sleep/sleep_unsafe.go:66-67 declares runtime.gopark with its Go 1.10 signature);
+# the per-packet burst calls need runtime.Pinner (Go 1.21) and say so in a build
+# constraint.
+FLOORS = {"checksum.go": (1, 10), "batch.go": (1, 10), "checksum_test.go": (1, 10),
+          "packets_go121.go": (1, 21), "packets_go121_test.go": (1, 21)}
+# APIs and syntax newer than Go 1.10, with the release that introduced them
+POST_110 = {
+    r"\bunsafe\.Slice\b": (1, 17), r"\bunsafe\.(Add|String|StringData|SliceData)\b": (1, 17),
+    r"\bruntime\.Pinner\b": (1, 21), r"\bany\b": (1, 18), r"\[\w+ (any|comparable)\]": (1, 18),
+    r"\b(min|max|clear)\(": (1, 21), r"\berrors\.(Is|As|Unwrap|Join)\b": (1, 13), r"%w": (1, 13),
+    r"\bstrings\.(Cut|Builder)\b": (1, 10), r"\b(os\.ReadFile|os\.WriteFile|io\.ReadAll)\b": (1, 16),
+    r"^//go:build": (1, 17), r"\bt\.(Cleanup|TempDir|Setenv)\(": (1, 14),
+}
+
+
+def _files(tests=False):
+    return sorted(f for f in glob.glob(os.path.join(GODIR, "*.go")) if tests or not f.endswith("_test.go"))
 
 
 def _go():
-    return open(GO).read()
+    """The package's non-test source, all files."""
+    return "\n".join(open(f).read() for f in _files())
+
+
+def test_every_go_file_has_a_floor():
+    assert {os.path.basename(f) for f in _files(tests=True)} == set(FLOORS)
+
+
+@pytest.mark.parametrize("name", sorted(FLOORS))
+def test_go_file_keeps_to_its_toolchain_floor(name):
+    src = open(os.path.join(GODIR, name)).read()
+    code = "\n".join(ln for ln in src.splitlines() if not ln.lstrip().startswith("//") or ln.startswith("//go:build"))
+    floor = FLOORS[name]
+    for pat, since in POST_110.items():
+        if since > floor:
+            assert not re.search(pat, code, re.M), f"{name} uses {pat} (Go {since[0]}.{since[1]}), floor {floor}"
+    if floor > (1, 10):  # newer than the callers' toolchain: excluded from it by a constraint
+        tag = f"go{floor[0]}.{floor[1]}"
+        assert src.startswith(f"//go:build {tag}\n// +build {tag}\n\npackage checksum"), name
+    else:
+        assert "+build" not in src and "//go:build" not in src, name
+
+
+def test_scalar_drop_in_stands_alone():
+    """checksum.go alone holds the reference's three functions and the #cgo flags;
+    packets_go121.go is the only user of runtime.Pinner."""
+    src = open(os.path.join(GODIR, "checksum.go")).read()
+    for sig in ("func Checksum(buf []byte, initial uint16) uint16",
+                "func PseudoHeaderChecksum(protocol uint32, srcAddr string, dstAddr string) uint16",
+                "func ChecksumCombine(a, b uint16) uint16"):
+        assert sig in src
+    assert "#cgo LDFLAGS" in src and "\"runtime\"" not in src
+    for f in _files(tests=True):
+        code = [ln for ln in open(f).read().splitlines() if not ln.lstrip().startswith("//")]
+        if any("runtime.Pinner" in ln for ln in code):
+            assert os.path.basename(f) == "packets_go121.go", f
 
 
 def test_go_calls_are_declared_and_exported():
@@ -36,8 +94,9 @@ def test_go_constants_are_defined():
         assert f"}} {t};" in hdr
 
 
-def test_cgo_preamble_compiles_as_c(tmp_path):
-    go = _go()
+@pytest.mark.parametrize("name", ["checksum.go", "batch.go", "packets_go121.go"])
+def test_cgo_preamble_compiles_as_c(tmp_path, name):
+    go = open(os.path.join(GODIR, name)).read()
     m = re.search(r"/\*\n(.*?)\*/\nimport \"C\"", go, re.S)
     assert m, "cgo preamble not found"
     pre = "\n".join(line for line in m.group(1).splitlines() if not line.startswith("#cgo"))

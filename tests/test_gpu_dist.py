@@ -97,8 +97,10 @@ def _rank(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_shards_on_hip_path_concatenate_to_oracle(dev, world):
+    """world 8 is the driver's SCALE shape (config 5: eight shards), here with the
+    eight ranks sharing cuda:0."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -107,7 +109,7 @@ def test_shards_on_hip_path_concatenate_to_oracle(dev, world):
     for p in procs:
         p.start()
     try:
-        ok, kernels, per = q.get(timeout=180)
+        ok, kernels, per = q.get(timeout=300)
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -133,6 +135,48 @@ def test_bench_self_launch_two_ranks_on_one_card(dev):
     assert all(p["GiB_s"] > 0 and p["kernel_avg_us"] > 0 for p in line["per_gpu"])
     assert line["config"]["backend"] == "gloo" and "SHARE" in line["config"]["parallelism"]
     assert line["config"]["kernel"] == "k_small<16,6>"
+
+
+def _bench_line(n, timeout):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                        "YU_BENCH_BACKEND")}
+    import time
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "20",
+                        "--warmup", "5", "--no-extra", "--no-e2e", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=timeout)
+    wall = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0]), wall
+
+
+def test_bench_self_launch_eight_ranks_on_one_card(dev):
+    """The driver's SCALE shape at N=8 (`bench.py --gpus 8`, no outer launcher),
+    rehearsed with the eight ranks sharing the one card over gloo: one line, eight
+    per_gpu entries, well inside a driver timeout."""
+    line, wall = _bench_line(8, 500)
+    print(f"bench --gpus 8 on one card: {wall:.1f} s, value {line['value']} GiB/s")
+    assert line["n_gpus"] == 8 and len(line["per_gpu"]) == 8
+    assert [p["rank"] for p in line["per_gpu"]] == list(range(8))
+    assert all(p["GiB_s"] > 0 and p["kernel_avg_us"] > 0 and p["device"] == 0 for p in line["per_gpu"])
+    assert line["config"]["backend"] == "gloo" and "SHARE" in line["config"]["parallelism"]
+    assert line["config"]["kernel"] == "k_small<16,6>"
+    assert wall < 300
+
+
+def test_launcher_device_count_matches_hip(dev):
+    """bench._device_count (KFD topology + render nodes, no HIP) against
+    torch.cuda.device_count() in a fresh process, with and without a visibility list."""
+    import bench
+    code = "import torch; print(torch.cuda.device_count())"
+    for extra in ({}, {"HIP_VISIBLE_DEVICES": "0"}):
+        env = dict(os.environ, **extra)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert bench._device_count(env) == int(r.stdout.strip().splitlines()[-1]), extra
 
 
 def _rccl_rank(port, q):

@@ -904,6 +904,50 @@ def test_kernel_verified_datagrams_on_gpu(dev):
         assert check(got), (mode, got)
 
 
+@pytest.mark.parametrize("n", [5000, 70000])
+def test_kernel_verified_datagrams_tiled_past_cutovers(dev, n):
+    """The kernel-verified datagrams drawn at random (seeded) into batches past the
+    4096-packet burst cut-over and past the 65536-packet chunk cut-over, so the default
+    pick is k_seg<8,dg/rx,c16> and k_seg<8,dg/rx> rather than k_loop: mixed start
+    alignments, headers across tile edges, 20-byte and optioned headers, and the
+    fields the Linux kernel accepted (or built) as the expected values."""
+    from test_kernel_verified import RX_OK, load, stored_fields
+    sb, so, kb, ko = load()
+    so, ko = so.astype(np.int64), ko.astype(np.int64)
+    z, want = stored_fields(sb, so)
+    rng = np.random.default_rng(n)
+
+    def tile(blob, offs, pick):
+        parts = [blob[offs[i]:offs[i + 1]] for i in pick]
+        o = np.zeros(len(parts) + 1, np.int64)
+        o[1:] = np.cumsum([len(p) for p in parts])
+        return np.concatenate(parts), o
+
+    pick = rng.integers(0, len(so) - 1, size=n)
+    zb, to = tile(z, so, pick)
+    sent, _ = tile(sb, so, pick)
+    want_t = want.reshape(-1, 2)[pick].ravel()
+    kname = batch.ragged_variant("tx_datagram", n)
+    assert kname.startswith("k_seg<8,dg") and (("c16" in kname) == (n < 65536)), kname
+    for base in (0, 1, 3):
+        pad = np.concatenate([np.zeros(base, np.uint8), zb, np.zeros(16, np.uint8)])
+        got = batch.checksum_ragged(_to(dev, pad), _to(dev, to + base), "tx_datagram").cpu().numpy()
+        assert np.array_equal(got, want_t), (base, np.nonzero(got != want_t)[0][:10])
+    d = _to(dev, np.concatenate([zb, np.zeros(16, np.uint8)]))
+    got = batch.checksum_ragged(d, _to(dev, to), "tx_datagram", fill=True).cpu().numpy()
+    assert np.array_equal(got, want_t)
+    assert np.array_equal(d.cpu().numpy()[:sent.size], sent)
+    # received: the sent and the kernel-built datagrams mixed
+    both = np.concatenate([sb, kb])
+    bo = np.concatenate([so[:-1], ko[:-1] + sb.size, [sb.size + kb.size]])
+    rb, ro = tile(both, bo, rng.integers(0, len(bo) - 1, size=n))
+    assert batch.ragged_variant("verify_rx", n).startswith("k_seg<8,rx")
+    for base in (0, 2):
+        pad = np.concatenate([np.zeros(base, np.uint8), rb, np.zeros(16, np.uint8)])
+        rx = batch.checksum_ragged(_to(dev, pad), _to(dev, ro + base), "verify_rx").cpu().numpy()
+        assert np.all(rx & RX_OK == RX_OK), (base, np.nonzero(rx & RX_OK != RX_OK)[0][:10])
+
+
 # ------------------------------------------------------------------ reference-executed vectors
 def test_refexec_vectors_on_gpu(dev):
     """The HIP path against known answers produced by executing the reference's own Go

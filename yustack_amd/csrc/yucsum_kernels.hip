@@ -1633,6 +1633,11 @@ __global__ __launch_bounds__(256, K == 3 ? 3 : 1) void k_seg(BatchArgs A) {
   // per-chunk state
   SegPt<Pos> pt[4];  // start, end, then (RX, DG) header and transport end
   SegRx rx;
+  // A header window that starts 4-aligned and crosses two tiles never gathers
+  // h[5] (its bytes lie past the 20-byte header), yet rx_parse reads it under a
+  // zero mask: give it a defined value once, not per chunk.
+#pragma unroll
+  for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
   // TX, DG: the checksum field's next unread byte (kNoPt: none or done; DG: the
   // transport field), the bytes of it still to read (2, or 1 when the field
   // straddles two tiles) and the address-ordered LE sum of those read:
