@@ -1,15 +1,18 @@
-# k_small fill with plain loads by default (fill_nt) vs HEAD (tools/old): kbench and the bench's config 9 line
+# round 4, call B: GPU suite on the tree with the 4-wave RX kind (SegChunk32, fused
+# park), kbench A/B against HEAD's library (tools/old), SQ counters for config 7
+# both ways, the driver-style bench line, trace + PMC passes of configs 7, 12, 13
 set -o pipefail
 mkdir -p gpurun_out
+T=r04b
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1 || { tail -60 gpurun_out/gpu_tests_$T.log; exit 1; }
+tail -2 gpurun_out/gpu_tests_$T.log
 O=LD_LIBRARY_PATH=tools/old
-bash tools/ab.sh "3 KB_FILL=1 $O" "3 KB_FILL=1" "3 KB_FILL=1 $O" "3 KB_FILL=1" "3 KB_FILL=1 $O" "3 KB_FILL=1" "3" "3 $O" > gpurun_out/kbench_ab_fill_nt2.log 2>&1 || { tail gpurun_out/kbench_ab_fill_nt2.log; exit 1; }
-python3 - <<'PY'
-import re,statistics,collections
-d=collections.defaultdict(list);cur=None
-for l in open('gpurun_out/kbench_ab_fill_nt2.log'):
-    if l.startswith('=='): cur=l[3:].strip(); continue
-    m=re.search(r'round \d+:\s+([\d.]+) us',l)
-    if m and cur: d[cur].append(float(m.group(1)))
-for k,v in d.items(): print(f"{k:45s} median {statistics.median(v):8.1f}  min {min(v):8.1f}  n={len(v)}")
-PY
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -k "fill" --timeout 120 --timeout-method thread 2>&1 | tail -1
+timeout -k 10 900 bash tools/ab.sh "16 $O" "16" "16 $O" "16" "16 $O" "16" "6 $O" "6" "5 $O" "5" "4 $O" "4" "15 $O" "15" "8 $O" "8" "3 $O" "3" "8 KB_FILL=1 KB_ALIGN4=1 $O" "8 KB_FILL=1 KB_ALIGN4=1" "15 KB_FILL=1 KB_ALIGN4=1 $O" "15 KB_FILL=1 KB_ALIGN4=1" > gpurun_out/kbench_ab_$T.log 2>&1 || { tail gpurun_out/kbench_ab_$T.log; exit 1; }
+grep -E "^==|round 2" gpurun_out/kbench_ab_$T.log
+TAG=_new bash tools/pmc_sq.sh 16 || exit 1
+TAG=_old bash tools/pmc_sq.sh 16 LD_LIBRARY_PATH=$R/tools/old || exit 1
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || { tail gpurun_out/bench_$T.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/bench_$T.json'));print(d['value'],d['roofline']['frac']);[print(k,v['kernel_avg_us'],v['roofline_frac']) for k,v in d['other_configs'].items()]"
+CFGS="7 12 13" timeout -k 10 600 bash tools/profile.sh $T || exit 1
+echo ok
