@@ -348,12 +348,16 @@ def test_tx_datagram_ragged(dev, oracle_c, npk):
     assert (rx[l4_def] & (O.RX_L4 | O.RX_L4_OK) == (O.RX_L4 | O.RX_L4_OK)).all()
 
 
+@pytest.mark.parametrize("shift", [0, 68])
 @pytest.mark.parametrize("npk", [5000, 70000])
 @pytest.mark.parametrize("mode,lo", [(O.MODE_UDP, 8), (O.MODE_TCP, 20), (O.MODE_ICMP, 4)])
-def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk):
+def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, shift):
     """In place on ragged small packets (4-aligned offsets, the fill contract) with a
     few large ones among them, in 16- and 64-packet k_seg chunks: only the fields
-    change, chunk edges included, and the results equal the oracle's."""
+    change, chunk edges included, and the results equal the oracle's. The TX kind's
+    whole-line write-back (YU_FILL_WB) stores the 128-byte lines of each chunk's last
+    tile; shift 68 starts the batch off a line boundary, so the first chunk's line
+    begins before the batch."""
     rng = np.random.default_rng(9900 + 7 * mode + npk)
     lens = (rng.integers(lo, 201, size=npk) + 3) & ~3
     lens[rng.choice(npk, size=npk // 500, replace=False)] = 4 * rng.integers(1000, 2500, size=npk // 500)
@@ -364,7 +368,9 @@ def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk):
         blob[offs[:-1].astype(np.int64) + 12] = 0x50
     addrs = _rand(rng, 8 * npk)
     want = oracle_c.batch(blob, mode, offsets=offs, addrs=addrs if mode != O.MODE_ICMP else None)
-    d = _to(dev, blob)
+    pre = _rand(rng, shift)
+    whole = _to(dev, np.concatenate([pre, blob]))
+    d = whole[shift:]
     got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), mode,
                                 addrs=_to(dev, addrs) if mode != O.MODE_ICMP else None, fill=True).cpu().numpy()
     assert np.array_equal(got, want)
@@ -375,6 +381,7 @@ def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk):
     exp[fi + 1] = (want & 0xFF).astype(np.uint8)
     bad = np.nonzero(d.cpu().numpy() != exp)[0]
     assert bad.size == 0, bad[:10]
+    assert np.array_equal(whole[:shift].cpu().numpy(), pre)  # the bytes before the batch
 
 
 def test_tx_datagram_fuzz(dev, oracle_c):

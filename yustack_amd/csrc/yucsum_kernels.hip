@@ -175,6 +175,17 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v) {
   return v;
 }
 
+// OR over the whole wave, in lane 63 (the same DPP steps as group_total<64>).
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // This wave's index in the grid's packet order. Blocks are dealt round-robin
 // over the 8 XCDs (blocks b and b+8 share an L2), so with xcd set the order is
 // swizzled to give each XCD a contiguous run of logical blocks: the one
@@ -1395,7 +1406,8 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
 
 // Wave-uniform geometry of a loaded chunk starting at packet p0 (waits for
 // its offsets). No such chunk: an empty range, so its loads are all masked.
-__device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk &k) {
+__device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk &k,
+                                         bool = false) {
   if (p0 >= n) {
     k.b0 = data & ~3ull;
     k.xe = 0;
@@ -1440,7 +1452,12 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
   if (SIDE) k.sd = load_side(sp, own ? i : n - 1);
 }
 
-__device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk32 &k) {
+// line128: the tiles start at the 128-byte line holding the chunk's first byte
+// (the in-place writer's whole-line write-back, k_seg), unless that line begins
+// before the batch; else at its dword. The bytes in front are loaded but lie
+// before every point, and the line was fetched for the previous chunk anyway.
+__device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk32 &k,
+                                         bool line128 = false) {
   if (p0 >= n) {
     k.b0 = data & ~3ull;
     k.xe = 0;
@@ -1450,8 +1467,9 @@ __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0,
   const uint64_t s0 = uniform64(k.s0);
   k.s0 = s0;
   const uint64_t s = data + s0;
-  k.b0 = s & ~3ull;
-  k.xe = (uint64_t)((uint32_t)__builtin_amdgcn_readlane((int)k.ey, 63) - (uint32_t)s0) + (s & 3u);
+  const uint64_t l = s & ~127ull;
+  k.b0 = line128 && l >= (data & ~3ull) ? l : s & ~3ull;
+  k.xe = (uint64_t)((uint32_t)__builtin_amdgcn_readlane((int)k.ey, 63) - (uint32_t)s0) + (s - k.b0);
 }
 
 // This lane's packet as (position relative to b0, length).
@@ -1465,7 +1483,7 @@ __device__ __forceinline__ void seg_xlen(const BatchArgs &A, const SegChunk &k, 
 template <int CH>
 __device__ __forceinline__ void seg_xlen(const BatchArgs &A, const SegChunk32 &k, uint32_t lane,
                                          uint64_t p0, uint32_t &x, uint32_t &len) {
-  const uint32_t h = (uint32_t)((uint64_t)(uintptr_t)A.data + k.s0) & 3u;  // b0's head bytes
+  const uint32_t h = (uint32_t)((uint64_t)(uintptr_t)A.data + k.s0 - k.b0);  // bytes before the chunk
   const uint32_t s0 = (uint32_t)k.s0;
   uint32_t ox;
   if (A.offsets) {  // back to back: the left neighbour's end
@@ -1696,6 +1714,11 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
   const uint64_t end = A.offsets ? data + A.offsets[A.n] : A.end;
   const uint32_t *s_dw = (const uint32_t *)s_data[wid];
   const bool contig = A.offsets != nullptr;  // ragged: packets back to back
+  // TX kind writing in place on a ragged batch: the fields go into the parked
+  // last tile of each chunk and its whole 128-byte lines are stored back (A.uf:
+  // 1 plain, 2 non-temporal stores; 0 = a 2-byte store per field). See the
+  // chunk epilogue.
+  const bool wbk = tx && A.fill && contig && A.uf != 0u;
   // Positions relative to the chunk's b0: 64-bit for the plain kind (RAW packets
   // up to YU_MAX_RAW_LEN), 32-bit for the TX / RX / DG kinds, whose packets are
   // at most 65535 bytes (include/yucsum.h), so a 64-packet chunk spans < 4.2 MB
@@ -1717,7 +1740,7 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
   Chunk cur, nxt;
   seg_load<CH, !RX>(A, sp, ch * CH, lane, cur);
   seg_load<CH, !RX>(A, sp, (ch + nwave) * CH, lane, nxt);
-  seg_geom(data, A.n, ch * CH, cur);
+  seg_geom(data, A.n, ch * CH, cur, wbk);
 
   // per-chunk state
   SegPt<Pos> pt[4];  // start, end, then (RX, DG) header and transport end
@@ -1780,7 +1803,7 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
     Chunk nn;  // the chunk after next: its loads go out before this
                   // step's tile loads, so waiting on them never waits on those
     if (last) {
-      seg_geom(data, A.n, (ch + nwave) * CH, nxt);
+      seg_geom(data, A.n, (ch + nwave) * CH, nxt, wbk);
       seg_load<CH, !RX>(A, sp, (ch + 2u * nwave) * CH, lane, nn);  // (RX, DG: no side data)
     }
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
@@ -1965,6 +1988,12 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
     const uint32_t pe = own_end ? pt[1].p : nx_p;
     const uint32_t te = own_end ? pt[1].t : nx_t;
     const uint64_t p = ch * CH + lane;
+    // TX in place (wbk): this lane's field offset in the tile (wf: it has one),
+    // its line when stored whole (64: not), its value
+    Pos wq = 0;
+    bool wf = false;
+    uint32_t wl = 64u, wr = 0u;
+    const Pos x0 = (Pos)__builtin_amdgcn_readlane((int)(uint32_t)pt[0].x, 0);  // the chunk's start
     if (lane < (uint32_t)CH && p < A.n) {
       const uint32_t odd = (uint32_t)pt[0].x & 1u;
       if (DG) {
@@ -2016,8 +2045,50 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
           v = le_to_be(pe - pt[0].p - (tx ? fsum : 0u), odd);
         }
         const uint64_t len = plen;
-        finish_packet(A, p, v, len, cur.sd, A.fill ? A.fill + (cur.b0 + pt[0].x - data) : nullptr,
-                      (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
+        uint8_t *pk = A.fill ? A.fill + (cur.b0 + pt[0].x - data) : nullptr;
+        if (tx && wbk && park && fld + 2u <= len) {
+          // the field's offset in the parked (last) tile, wrapping below it;
+          // its line is stored whole below when the field lies in one line of
+          // this tile that holds no byte outside this chunk
+          wq = pt[0].x + fld - tb;
+          wf = true;
+          const Pos ls = wq & ~(Pos)127;
+          if (wq + 2u <= T && (wq & 127u) != 127u && tb + ls >= x0 && tb + ls + 128u <= cur.xe) {
+            wl = (uint32_t)wq >> 7;
+            pk = nullptr;  // no 2-byte store
+          }
+        }
+        const uint32_t r = packet_value(A, v, len, cur.sd);
+        if (A.out) A.out[p] = (uint16_t)r;
+        wr = r;
+        if (pk) store_field(A, r, pk, (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
+      }
+    }
+    if (tx && wbk && park) {  // wave-uniform: the in-place write-back
+      // 1. Every field byte that lies in the tile goes into its parked copy, the
+      //    ones left to their 2-byte stores too (same bytes: a line stored whole
+      //    that holds one stays right).
+      uint8_t *sb = (uint8_t *)s_data[wid];
+      if (wf && wq < T) sb[wq] = (uint8_t)(wr >> 8);
+      if (wf && wq + 1u < T) sb[wq + 1u] = (uint8_t)wr;  // (wq + 1 == 0: a field from the tile before)
+      // 2. The lines holding a field of their own, as a 64-bit mask (T / 128 <= 64 lines).
+      const uint64_t m = (uint64_t)wave_or(wl < 32u ? 1u << wl : 0u) |
+                         ((uint64_t)wave_or(wl >= 32u && wl < 64u ? 1u << (wl - 32u) : 0u) << 32);
+      wave_lds_fence();
+      // 3. Those lines from the tile copy, as full-line 16-byte stores (8 lanes
+      //    per line, one contiguous KiB per instruction). Memory then sees whole
+      //    lines, not one partial write per field.
+      const __amdgpu_buffer_rsrc_t wr_r = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(A.fill + (cur.b0 + tb - data)), (short)0, (int)T, 0x00020000);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t k = (uint32_t)u * 64u + lane;
+        const uint4 d = s_data[wid][k];
+        const uint32_t off = ((m >> (k >> 3)) & 1u) ? 16u * k : kOOB;
+        if (A.uf == 2u)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 2);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 0);
       }
     }
     if ((ch + nwave) * CH >= A.n) return true;
@@ -2420,6 +2491,14 @@ int fill_nt() {
   return v;
 }
 
+// The ragged in-place writer of k_seg's TX kind (wbk): 0 = one 2-byte store per
+// field; 1 = the fields patched into the parked tile and their 128-byte lines
+// stored whole; 2 = the same with non-temporal stores. YU_FILL_WB overrides.
+int fill_wb() {
+  static int v = env_int("YU_FILL_WB", 0, 2, 2);
+  return v;
+}
+
 // YU_XCD: 1 = XCD-aware block order (grid_wave), 0 (default) = plain blockIdx.
 // Measured (round 1, tools/ab.sh): no gain on any config — these kernels
 // share at most one line between neighbouring blocks, and the Infinity Cache
@@ -2546,7 +2625,7 @@ int batch_ragged(const uint8_t *data, uint8_t *fill, const uint64_t *offsets,
   A.end = 0;
   A.len = 0;
   A.initial = initial;
-  A.uf = 0;
+  A.uf = fill && mode_is_tx(mode) ? (uint32_t)fill_wb() : 0u;  // k_seg TX kind: the write-back
   A.mode = mode;
   // k_seg streams the batch's bytes (exact BE recovery for chunks holding a
   // RAW packet > 131072 bytes); k_rag takes the IPv4 header-only modes.
