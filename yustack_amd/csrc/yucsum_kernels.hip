@@ -175,7 +175,8 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v) {
   return v;
 }
 
-// OR over the whole wave, in lane 63 (the same DPP steps as group_total<64>).
+// OR over the whole wave, in every lane (the same DPP steps as group_total<64>,
+// then lane 63's value handed round in a VGPR: the caller is short of SGPRs).
 __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
   v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
   v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
@@ -183,7 +184,7 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
   v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
   v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
   v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  return (uint32_t)__shfl((int)v, 63, 64);
 }
 
 // This wave's index in the grid's packet order. Blocks are dealt round-robin
@@ -1715,9 +1716,9 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
   const uint32_t *s_dw = (const uint32_t *)s_data[wid];
   const bool contig = A.offsets != nullptr;  // ragged: packets back to back
   // TX kind writing in place on a ragged batch: the fields go into the parked
-  // last tile of each chunk and its whole 128-byte lines are stored back (A.uf:
-  // 1 plain, 2 non-temporal stores; 0 = a 2-byte store per field). See the
-  // chunk epilogue.
+  // last tile of each chunk and its whole 128-byte lines are stored back with
+  // non-temporal stores (A.uf != 0; 0 = a 2-byte store per field). See the chunk
+  // epilogue.
   const bool wbk = tx && A.fill && contig && A.uf != 0u;
   // Positions relative to the chunk's b0: 64-bit for the plain kind (RAW packets
   // up to YU_MAX_RAW_LEN), 32-bit for the TX / RX / DG kinds, whose packets are
@@ -1993,7 +1994,7 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
     Pos wq = 0;
     bool wf = false;
     uint32_t wl = 64u, wr = 0u;
-    const Pos x0 = (Pos)__builtin_amdgcn_readlane((int)(uint32_t)pt[0].x, 0);  // the chunk's start
+    const Pos x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);  // the chunk's start
     if (lane < (uint32_t)CH && p < A.n) {
       const uint32_t odd = (uint32_t)pt[0].x & 1u;
       if (DG) {
@@ -2085,10 +2086,7 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
         const uint32_t k = (uint32_t)u * 64u + lane;
         const uint4 d = s_data[wid][k];
         const uint32_t off = ((m >> (k >> 3)) & 1u) ? 16u * k : kOOB;
-        if (A.uf == 2u)
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 2);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 2);  // nt
       }
     }
     if ((ch + nwave) * CH >= A.n) return true;
@@ -2493,9 +2491,9 @@ int fill_nt() {
 
 // The ragged in-place writer of k_seg's TX kind (wbk): 0 = one 2-byte store per
 // field; 1 = the fields patched into the parked tile and their 128-byte lines
-// stored whole; 2 = the same with non-temporal stores. YU_FILL_WB overrides.
+// stored whole. YU_FILL_WB overrides.
 int fill_wb() {
-  static int v = env_int("YU_FILL_WB", 0, 2, 2);
+  static int v = env_int("YU_FILL_WB", 0, 1, 1);
   return v;
 }
 
