@@ -2054,7 +2054,9 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
           wq = pt[0].x + fld - tb;
           wf = true;
           const Pos ls = wq & ~(Pos)127;
-          if (wq + 2u <= T && (wq & 127u) != 127u && tb + ls >= x0 && tb + ls + 128u <= cur.xe) {
+          // (wq wraps for a field in an earlier tile: wq <= T - 2 keeps those out,
+          // a field ending right at this tile's start included)
+          if (wq <= T - 2u && (wq & 127u) != 127u && tb + ls >= x0 && tb + ls + 128u <= cur.xe) {
             wl = (uint32_t)wq >> 7;
             pk = nullptr;  // no 2-byte store
           }
