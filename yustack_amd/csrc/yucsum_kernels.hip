@@ -1407,8 +1407,12 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
 
 // Wave-uniform geometry of a loaded chunk starting at packet p0 (waits for
 // its offsets). No such chunk: an empty range, so its loads are all masked.
+// line128: the tiles start at the 128-byte line holding the chunk's first byte
+// (the in-place writer's whole-line write-back, k_seg), unless that line begins
+// before the batch; else at its dword. The bytes in front are loaded but lie
+// before every point, and the line was fetched for the previous chunk anyway.
 __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk &k,
-                                         bool = false) {
+                                         bool line128 = false) {
   if (p0 >= n) {
     k.b0 = data & ~3ull;
     k.xe = 0;
@@ -1416,86 +1420,9 @@ __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0,
   }
   const uint64_t s = data + readlane64(k.ox, 0);
   const uint64_t e = data + readlane64(k.oy, 63);  // lane 63's end = the chunk end
-  k.b0 = s & ~3ull;
-  k.xe = e - k.b0;
-}
-
-// The 32-bit kinds (TX / RX / DG: packets <= 65535 bytes, so a chunk spans
-// < 4.2 MB) keep a loaded chunk in fewer registers: each lane holds only the low
-// dword of its packet's end offset, and the chunk's first offset is one 8-byte
-// value all lanes load alike (read to SGPRs by seg_geom). A lane's start is its
-// left neighbour's end (ragged batches lie back to back) or i * stride
-// (uniform); every position and length is a 32-bit difference from the first
-// offset. Per chunk in flight: 3 VGPRs instead of 4 (two 64-bit offsets).
-struct SegChunk32 {
-  uint32_t ey;  // low dword of this lane's packet end (lanes past the batch or
-                // the chunk: the chunk end)
-  uint64_t s0;  // the chunk's first offset (ragged: offsets[p0]; uniform: p0 * stride)
-  uint64_t b0;  // floor4 address of the chunk's first byte (wave-uniform)
-  uint64_t xe;  // chunk end relative to b0 (wave-uniform)
-  Side sd;
-};
-
-template <int CH, bool SIDE = true>
-__device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
-                                         uint64_t p0, uint32_t lane, SegChunk32 &k) {
-  const uint64_t n = A.n;
-  const uint64_t i = p0 + lane;
-  const uint64_t ce = p0 < n ? (n - p0 < (uint64_t)CH ? n : p0 + CH) : n;
-  const bool own = lane < (uint32_t)CH && i < n;
-  const uint64_t last = p0 < n ? ce - 1u : 0u;
-  const uint32_t *lo = A.offsets ? (const uint32_t *)A.offsets : g_side_zero;  // little-endian
-  const uint32_t ry = lo[A.offsets ? 2u * (own ? i + 1 : ce) : 0];
-  const uint64_t *offs = A.offsets ? A.offsets : (const uint64_t *)g_side_zero;
-  const uint64_t r0 = offs[A.offsets ? (p0 < n ? p0 : n) : 0];
-  k.ey = A.offsets ? ry : (uint32_t)((own ? i : last) * A.stride + A.len);
-  k.s0 = A.offsets ? r0 : (p0 < n ? p0 : 0u) * A.stride;
-  if (SIDE) k.sd = load_side(sp, own ? i : n - 1);
-}
-
-// line128: the tiles start at the 128-byte line holding the chunk's first byte
-// (the in-place writer's whole-line write-back, k_seg), unless that line begins
-// before the batch; else at its dword. The bytes in front are loaded but lie
-// before every point, and the line was fetched for the previous chunk anyway.
-__device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk32 &k,
-                                         bool line128 = false) {
-  if (p0 >= n) {
-    k.b0 = data & ~3ull;
-    k.xe = 0;
-    k.s0 = 0;
-    return;
-  }
-  const uint64_t s0 = uniform64(k.s0);
-  k.s0 = s0;
-  const uint64_t s = data + s0;
   const uint64_t l = s & ~127ull;
   k.b0 = line128 && l >= (data & ~3ull) ? l : s & ~3ull;
-  k.xe = (uint64_t)((uint32_t)__builtin_amdgcn_readlane((int)k.ey, 63) - (uint32_t)s0) + (s - k.b0);
-}
-
-// This lane's packet as (position relative to b0, length).
-template <int CH>
-__device__ __forceinline__ void seg_xlen(const BatchArgs &A, const SegChunk &k, uint32_t,
-                                         uint64_t, uint64_t &x, uint64_t &len) {
-  x = (uint64_t)(uintptr_t)A.data + k.ox - k.b0;
-  len = k.oy - k.ox;
-}
-
-template <int CH>
-__device__ __forceinline__ void seg_xlen(const BatchArgs &A, const SegChunk32 &k, uint32_t lane,
-                                         uint64_t p0, uint32_t &x, uint32_t &len) {
-  const uint32_t h = (uint32_t)((uint64_t)(uintptr_t)A.data + k.s0 - k.b0);  // bytes before the chunk
-  const uint32_t s0 = (uint32_t)k.s0;
-  uint32_t ox;
-  if (A.offsets) {  // back to back: the left neighbour's end
-    const uint32_t l = (uint32_t)__shfl((int)k.ey, (int)(lane ? lane - 1u : 0u), 64);
-    ox = lane ? l : s0;
-  } else {  // lanes past the batch sit at the chunk end (ey)
-    const bool own = lane < (uint32_t)CH && p0 + lane < A.n;
-    ox = own ? (uint32_t)((p0 + lane) * A.stride) : k.ey;
-  }
-  x = ox - s0 + h;
-  len = k.ey - ox;
+  k.xe = e - k.b0;
 }
 
 // Loads of tile t (bytes [t*T, t*T + T) past b0) of a chunk ending xe past
@@ -1532,17 +1459,6 @@ __device__ __forceinline__ uint32_t seg_part(const uint4 &d, uint32_t r) {
     acc = BYTES ? __builtin_amdgcn_sad_u8(x, 0u, acc) : sad(x, acc);
   }
   return acc;
-}
-
-// The LE sum of the first r (0..15) bytes of a 16-byte chunk, from the chunk's
-// dword prefix sums: 3 sad, 6 selects and one masked sad (seg_part's per-dword
-// masks take about twice the VALU).
-__device__ __forceinline__ uint32_t seg_part_le(const uint4 &d, uint32_t r) {
-  const uint32_t w = r >> 2;
-  const uint32_t s1 = sad(d.x, 0u), s2 = sad(d.y, s1), s3 = sad(d.z, s2);
-  const uint32_t base = w == 0u ? 0u : (w == 1u ? s1 : (w == 2u ? s2 : s3));
-  const uint32_t dw = w == 0u ? d.x : (w == 1u ? d.y : (w == 2u ? d.z : d.w));
-  return sad(dw & ((1u << (8u * (r & 3u))) - 1u), base);
 }
 
 // P (or T, BYTES) at tile offset q from the parked tile: the exclusive prefix at
@@ -1685,14 +1601,10 @@ __device__ __forceinline__ uint64_t seg_waves(const BatchArgs &A) {
 // the transport field's two bytes are read from the tile that holds them).
 constexpr int kSegPlain = 0, kSegTx = 1, kSegRx = 2, kSegDg = 3;
 
-// Occupancy. The RX kind (small received datagrams, bench config 7) is asked
-// for 4 waves per SIMD: <= 128 VGPRs (SegChunk32, the park fused into the scan)
-// and 40 KiB of LDS per block (16-byte chunk prefixes, read back with
-// seg_part_le, instead of half-chunk ones), so 4 blocks fit a CU. The DG kind
-// asks for 3, which it would otherwise miss by a few VGPRs; the others are left
-// alone.
+// (the DG kind asks for at least 3 waves per SIMD, which it would otherwise
+// miss by a few VGPRs; the other kinds are left alone)
 template <int U, int NT, int K, int CH = 64>
-__global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void k_seg(BatchArgs A) {
+__global__ __launch_bounds__(256, K == kSegTx || K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   constexpr bool DG = K == kSegDg;
   constexpr bool RX = K == kSegRx || DG;  // parses each packet's IPv4 header
   constexpr bool tx = K == kSegTx;
@@ -1701,9 +1613,9 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
   constexpr uint32_t T = 64u * 16u * U;
   constexpr uint32_t NC = 64u * U;  // chunks per tile
   __shared__ uint4 s_data[4][NC];   // the tile's bytes
-  // exclusive prefixes per 16-byte chunk (plain kind: L, then T; RX kind) or per
-  // 8-byte half chunk (TX, DG: seg_point)
-  __shared__ uint32_t s_pre[4][K == kSegPlain || K == kSegRx ? NC : 2 * NC];
+  // exclusive prefixes per 16-byte chunk (plain kind: L, then T) or per 8-byte half
+  // chunk (the others, seg_point)
+  __shared__ uint32_t s_pre[4][K == kSegPlain ? NC : 2 * NC];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t wave = grid_wave(A.xcd);
@@ -1729,16 +1641,14 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
   // CH < 64: lane CH holds no packet but sits at the chunk's end, so its start
   // point is the chunk's end point and every packet's end is its successor's start
   constexpr bool kMarker = CH < 64;
-  // points from half-chunk prefixes (seg_point): the TX and DG kinds; the plain
-  // kind's registers (exact path) leave no room for the halves' sums, and the RX
-  // kind keeps its LDS to 40 KiB per block (see the launch bounds)
-  constexpr bool HP = K == kSegTx || K == kSegDg;
+  // points from half-chunk prefixes (seg_point): the 32-bit kinds; the plain
+  // kind's registers (exact path) leave no room for the halves' sums
+  constexpr bool HP = K != kSegPlain;
   constexpr Pos kNoPt = ~(Pos)0;             // a point slot not in use
 
   uint64_t ch = wave;
   if (wave >= nwave || ch * CH >= A.n) return;
-  using Chunk = typename std::conditional<K == kSegPlain, SegChunk, SegChunk32>::type;
-  Chunk cur, nxt;
+  SegChunk cur, nxt;
   seg_load<CH, !RX>(A, sp, ch * CH, lane, cur);
   seg_load<CH, !RX>(A, sp, (ch + nwave) * CH, lane, nxt);
   seg_geom(data, A.n, ch * CH, cur, wbk);
@@ -1746,6 +1656,11 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
   // per-chunk state
   SegPt<Pos> pt[4];  // start, end, then (RX, DG) header and transport end
   SegRx rx;
+  // A header window that starts 4-aligned and crosses two tiles never gathers
+  // h[5] (its bytes lie past the 20-byte header), yet rx_parse reads it under a
+  // zero mask: give it a defined value once, not per chunk.
+#pragma unroll
+  for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
   // A header window that starts 4-aligned and crosses two tiles never gathers
   // h[5] (its bytes lie past the 20-byte header), yet rx_parse reads it under a
   // zero mask: give it a defined value once, not per chunk.
@@ -1759,12 +1674,10 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
   uint32_t fk = 0, fsum = 0;
   bool exact = false;
   uint32_t carry_l = 0, carry_t = 0;
-  Pos plen = 0;  // this lane's packet length in the current chunk
-  auto begin_chunk = [&](const Chunk &k, uint64_t p0) __attribute__((always_inline)) {
-    Pos x, len;
-    seg_xlen<CH>(A, k, lane, p0, x, len);
-    plen = len;
-    const Pos y = x + len;
+  auto begin_chunk = [&](const SegChunk &k) __attribute__((always_inline)) {
+    const Pos x = (Pos)(data + k.ox - k.b0);
+    const Pos y = (Pos)(data + k.oy - k.b0);
+    const uint64_t len = k.oy - k.ox;
     pt[0].x = x;
     // ragged packets lie back to back: P(end) is the next lane's P(start), so
     // only lane 63 evaluates an end point (the chunk end); RX needs none
@@ -1792,7 +1705,7 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
     exact = K == kSegPlain && mode == YU_MODE_RAW && __any((int)(len > kLEMax));
     carry_l = carry_t = 0u;
   };
-  begin_chunk(cur, ch * CH);
+  begin_chunk(cur);
 
   uint64_t t = 0;
   // One tile: issue the loads of the next item into cn, then sum c.
@@ -1801,7 +1714,7 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
     // the chunk's tiles cover [0, xe); a point at a tile's end (xe itself,
     // when tile-aligned) takes the running sums after that tile
     const bool last = t * T + T >= cur.xe;  // wave-uniform
-    Chunk nn;  // the chunk after next: its loads go out before this
+    SegChunk nn;  // the chunk after next: its loads go out before this
                   // step's tile loads, so waiting on them never waits on those
     if (last) {
       seg_geom(data, A.n, (ch + nwave) * CH, nxt, wbk);
@@ -1810,38 +1723,17 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
                           end, cn);
 
-    // does a packet boundary (or header) lie in this tile? Then the tile's bytes
-    // and prefixes are parked in LDS as the scan produces them (no prefix array
-    // held across the scan)
-    const Pos tb = (Pos)(t * T);
-    bool here = false;
-#pragma unroll
-    for (int i = 0; i < NP; ++i)
-      if (!(RX && i == 1)) here |= pt[i].x - tb < T;  // (RX and DG have no end point)
-    if (FB) here |= fx - tb < T;
-    if (RX) {  // a header window [floor4(start), +24) still being gathered
-      const Pos hs = pt[0].x & ~(Pos)3;
-      here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
-    }
-    const bool park = __any((int)here);
-
     // chunk sums, address-ordered exclusive prefixes (DPP scan per u)
-    uint32_t ptt[U];
+    const Pos tb = (Pos)(t * T);
+    // chunk prefix; HP: also the chunk's first half's sum (half-chunk prefixes)
+    uint32_t pl[U], ph[U], ptt[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      // HP: also the chunk's first half's sum (half-chunk prefixes)
-      const uint32_t ph = sad(c[u].y, sad(c[u].x, 0u));
-      const uint32_t s = sad(c[u].w, sad(c[u].z, ph));
+      ph[u] = sad(c[u].y, sad(c[u].x, 0u));
+      const uint32_t s = sad(c[u].w, sad(c[u].z, ph[u]));
       const uint32_t inc = group_total<64>(s);
-      const uint32_t pl = carry_l + inc - s;
+      pl[u] = carry_l + inc - s;
       carry_l += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-      if (park) {
-        s_data[wid][u * 64 + lane] = c[u];
-        if (HP)
-          ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl, pl + ph);
-        else
-          s_pre[wid][u * 64 + lane] = pl;
-      }
     }
     if (exact) {
 #pragma unroll
@@ -1855,7 +1747,25 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
         carry_t += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
       }
     }
-    if (park) {
+    bool here = false;
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+      if (!(RX && i == 1)) here |= pt[i].x - tb < T;  // (RX and DG have no end point)
+    if (FB) here |= fx - tb < T;
+    if (RX) {  // a header window [floor4(start), +24) still being gathered
+      const Pos hs = pt[0].x & ~(Pos)3;
+      here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
+    }
+    const bool park = __any((int)here);
+    if (park) {  // a packet boundary (or header) lies in this tile
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        s_data[wid][u * 64 + lane] = c[u];
+        if (HP)
+          ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl[u], pl[u] + ph[u]);
+        else
+          s_pre[wid][u * 64 + lane] = pl[u];
+      }
       __builtin_amdgcn_wave_barrier();
       bool parsed = false;
       if (RX && rx.need) {  // gather header dwords held by this tile, parse
@@ -1879,12 +1789,12 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
         }
         if (rx.need == 0u) {
           uint32_t hl, tl;
-          rx_parse(rx, (uint32_t)pt[0].x & 3u, plen, hl, tl);
+          rx_parse(rx, (uint32_t)pt[0].x & 3u, cur.oy - cur.ox, hl, tl);
           // a well-formed datagram fills its packet: in a ragged chunk its
           // transport end is the next lane's start (the marker lane's, for the
           // chunk's last packet), already evaluated; when every lane's is, the
           // wave skips the transport-end slot altogether
-          rx.tnext = contig && kMarker && tl == (uint32_t)plen ? 1u : 0u;
+          rx.tnext = contig && kMarker && tl == (uint32_t)(cur.oy - cur.ox) ? 1u : 0u;
           if (DG) {
             // in contract HeaderLength() >= 20: every point lies at or past
             // byte 20, so never in a tile that has gone by
@@ -1912,8 +1822,7 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
             pt[i].p = seg_point<false>(s_pre[wid], (const uint2 *)s_data[wid], (uint32_t)q);
           } else {
             const uint32_t k = (uint32_t)q >> 4;
-            pt[i].p = K == kSegRx ? seg_part_le(s_data[wid][k], (uint32_t)q & 15u) + s_pre[wid][k]
-                                  : s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
+            pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
           }
         }
       }
@@ -1994,7 +1903,7 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
     Pos wq = 0;
     bool wf = false;
     uint32_t wl = 64u, wr = 0u;
-    const Pos x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);  // the chunk's start
+    const Pos x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);  // the chunk's start (wbk: 32-bit)
     if (lane < (uint32_t)CH && p < A.n) {
       const uint32_t odd = (uint32_t)pt[0].x & 1u;
       if (DG) {
@@ -2016,9 +1925,8 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
           }
         }
         if (A.fill) {
-          uint8_t *pk = A.fill + (cur.b0 + pt[0].x - data);
-          if (rx.hl) put_be16(pk + 10u, ip);
-          if (rx.fo) put_be16(pk + rx.fo, l4);
+          if (rx.hl) put_be16(A.fill + cur.ox + 10u, ip);
+          if (rx.fo) put_be16(A.fill + cur.ox + rx.fo, l4);
         }
       } else if (RX) {
         // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
@@ -2045,8 +1953,8 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
         } else {
           v = le_to_be(pe - pt[0].p - (tx ? fsum : 0u), odd);
         }
-        const uint64_t len = plen;
-        uint8_t *pk = A.fill ? A.fill + (cur.b0 + pt[0].x - data) : nullptr;
+        const uint64_t len = cur.oy - cur.ox;
+        uint8_t *pk = A.fill ? A.fill + cur.ox : nullptr;
         if (tx && wbk && park && fld + 2u <= len) {
           // the field's offset in the parked (last) tile, wrapping below it;
           // its line is stored whole below when the field lies in one line of
@@ -2079,11 +1987,13 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
                          ((uint64_t)wave_or(wl >= 32u && wl < 64u ? 1u << (wl - 32u) : 0u) << 32);
       wave_lds_fence();
       // 3. Those lines from the tile copy, as full-line 16-byte stores (8 lanes
-      //    per line, one contiguous KiB per instruction). Memory then sees whole
-      //    lines, not one partial write per field.
+      //    per line, one contiguous KiB per instruction), non-temporal. Memory
+      //    then sees whole lines, not one partial write per field.
       const __amdgpu_buffer_rsrc_t wr_r = __builtin_amdgcn_make_buffer_rsrc(
           (void *)(A.fill + (cur.b0 + tb - data)), (short)0, (int)T, 0x00020000);
-#pragma unroll
+      // (one 16-byte LDS read in flight per store: the next tile's loads hold
+      // 32 VGPRs here, and the TX kind must stay within 168)
+#pragma unroll 1
       for (int u = 0; u < U; ++u) {
         const uint32_t k = (uint32_t)u * 64u + lane;
         const uint4 d = s_data[wid][k];
@@ -2095,7 +2005,7 @@ __global__ __launch_bounds__(256, K == kSegRx ? 4 : (K == kSegDg ? 3 : 1)) void 
     cur = nxt;
     nxt = nn;
     ch += nwave;
-    begin_chunk(cur, ch * CH);
+    begin_chunk(cur);
     t = 0;
     return false;
   };
@@ -2504,12 +2414,10 @@ int fill_wb() {
 // share at most one line between neighbouring blocks, and the Infinity Cache
 // already absorbs its second fetch — and -1..3 % on configs 2/3, so it is off.
 // YU_SEG_SMALL_BLOCKS: blocks per CU that work on a small-packet ragged
-// batch (seg_waves); 0 = the whole grid. Default 3, and 4 for the RX kind,
-// whose 40 KiB of LDS and <= 128 VGPRs per lane let 4 blocks (4 waves per SIMD)
-// be resident; the other 8 KiB-tile kinds fit 3.
-int seg_small_blocks(bool rx) {
-  static int v = env_int("YU_SEG_SMALL_BLOCKS", 0, 64, -1);
-  return v >= 0 ? v : (rx ? 4 : 3);
+// batch (seg_waves); 0 = the whole grid.
+int seg_small_blocks() {
+  static int v = env_int("YU_SEG_SMALL_BLOCKS", 0, 64, 3);
+  return v;
 }
 
 int use_xcd() {
@@ -2545,8 +2453,7 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   if (blocks < 1) blocks = 1;
   BatchArgs a = A;
   a.xcd = (uint32_t)use_xcd();
-  const bool rx4 = &v == &kSegRx8 || &v == &kSegRx8c16;
-  a.small_waves = (uint32_t)cu_count(dev) * 4u * (uint32_t)seg_small_blocks(rx4);
+  a.small_waves = (uint32_t)cu_count(dev) * 4u * (uint32_t)seg_small_blocks();
   KernelFn k = A.fill && v.fill ? v.fill : v.fn[use_nt()];
   if (v.run && !runs) k = v.inter[A.fill ? fill_nt() : use_nt()];
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
