@@ -1,20 +1,19 @@
-# round 4, call C: the round-start k_seg plus the TX kind's whole-line in-place
-# write-back (the 4-wave RX variant reverted): GPU suite, the fill tests with the
-# write-back off, kbench A/B against the round-start library (tools/old), the
-# driver-style bench line, trace + PMC passes of configs 12 and 13
+# round 4, call D: k_seg with the RX kind's one-tile straight-line path, the TX kind
+# on 32-bit chunk loads with the park fused into its scan (and the whole-line
+# in-place write-back): GPU suite, fill tests with the write-back off, kbench A/B
+# against the round-start library (tools/old), the driver-style bench line
 set -o pipefail
 mkdir -p gpurun_out
-T=r04c
+T=r04d
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1 || { tail -60 gpurun_out/gpu_tests_$T.log; exit 1; }
 tail -1 gpurun_out/gpu_tests_$T.log
 YU_FILL_WB=0 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "fill or fuzz or kernel_verified" --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_${T}_wb0.log 2>&1 || { tail -40 gpurun_out/gpu_tests_${T}_wb0.log; exit 1; }
 tail -1 gpurun_out/gpu_tests_${T}_wb0.log
 O=LD_LIBRARY_PATH=tools/old
 F="KB_FILL=1 KB_ALIGN4=1"
-timeout -k 10 900 bash tools/ab.sh "16 $O" "16" "16 $O" "16" "15 $O" "15" "15 $O" "15" "8 $O" "8" "8 $O" "8" "4 $O" "4" \
-  "8 $F $O" "8 $F" "8 $F $O" "8 $F" "8 $F YU_FILL_WB=0" "7 $F $O" "7 $F" > gpurun_out/kbench_ab_$T.log 2>&1 || { tail gpurun_out/kbench_ab_$T.log; exit 1; }
+timeout -k 10 900 bash tools/ab.sh "16 $O" "16" "16 $O" "16" "16 $O" "16" "8 $O" "8" "8 $O" "8" "6 $O" "6" "5 $O" "5" "4 $O" "4" \
+  "15 $O" "15" "15 KB_MODE=8 $O" "15 KB_MODE=8" "8 $F $O" "8 $F" "8 $F $O" "8 $F" "7 $F $O" "7 $F" > gpurun_out/kbench_ab_$T.log 2>&1 || { tail gpurun_out/kbench_ab_$T.log; exit 1; }
 grep -E "^==|round 2" gpurun_out/kbench_ab_$T.log
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || { tail gpurun_out/bench_$T.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/bench_$T.json'));print(d['value'],d['roofline']['frac']);[print(k,v['kernel_avg_us'],v['roofline_frac']) for k,v in d['other_configs'].items()]"
-CFGS="12 13" timeout -k 10 600 bash tools/profile.sh $T || exit 1
 echo ok

@@ -1425,6 +1425,81 @@ __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0,
   k.xe = e - k.b0;
 }
 
+// The TX kind (UDP / TCP / ICMP fields: packets <= 65535 bytes, so a chunk spans
+// < 4.2 MB) keeps a loaded chunk in fewer registers, which its in-place
+// write-back needs: each lane holds only the low dword of its packet's end
+// offset, and the chunk's first offset is one 8-byte value all lanes load alike
+// (read to SGPRs by seg_geom). A lane's start is its left neighbour's end
+// (ragged batches lie back to back) or i * stride (uniform); every position and
+// length is a 32-bit difference from the first offset. Per chunk in flight: 3
+// VGPRs instead of 4 (two 64-bit offsets).
+struct SegChunk32 {
+  uint32_t ey;  // low dword of this lane's packet end (lanes past the batch or
+                // the chunk: the chunk end)
+  uint64_t s0;  // the chunk's first offset (ragged: offsets[p0]; uniform: p0 * stride)
+  uint64_t b0;  // address the chunk's tiles start at (wave-uniform, see seg_geom)
+  uint64_t xe;  // chunk end relative to b0 (wave-uniform)
+  Side sd;
+};
+
+template <int CH, bool SIDE = true>
+__device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
+                                         uint64_t p0, uint32_t lane, SegChunk32 &k) {
+  const uint64_t n = A.n;
+  const uint64_t i = p0 + lane;
+  const uint64_t ce = p0 < n ? (n - p0 < (uint64_t)CH ? n : p0 + CH) : n;
+  const bool own = lane < (uint32_t)CH && i < n;
+  const uint64_t last = p0 < n ? ce - 1u : 0u;
+  const uint32_t *lo = A.offsets ? (const uint32_t *)A.offsets : g_side_zero;  // little-endian
+  const uint32_t ry = lo[A.offsets ? 2u * (own ? i + 1 : ce) : 0];
+  const uint64_t *offs = A.offsets ? A.offsets : (const uint64_t *)g_side_zero;
+  const uint64_t r0 = offs[A.offsets ? (p0 < n ? p0 : n) : 0];
+  k.ey = A.offsets ? ry : (uint32_t)((own ? i : last) * A.stride + A.len);
+  k.s0 = A.offsets ? r0 : (p0 < n ? p0 : 0u) * A.stride;
+  if (SIDE) k.sd = load_side(sp, own ? i : n - 1);
+}
+
+__device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk32 &k,
+                                         bool line128 = false) {
+  if (p0 >= n) {
+    k.b0 = data & ~3ull;
+    k.xe = 0;
+    k.s0 = 0;
+    return;
+  }
+  const uint64_t s0 = uniform64(k.s0);
+  k.s0 = s0;
+  const uint64_t s = data + s0;
+  const uint64_t l = s & ~127ull;
+  k.b0 = line128 && l >= (data & ~3ull) ? l : s & ~3ull;
+  k.xe = (uint64_t)((uint32_t)__builtin_amdgcn_readlane((int)k.ey, 63) - (uint32_t)s0) + (s - k.b0);
+}
+
+// This lane's packet as (position relative to b0, length).
+template <int CH>
+__device__ __forceinline__ void seg_xlen(const BatchArgs &A, const SegChunk &k, uint32_t,
+                                         uint64_t, uint64_t &x, uint64_t &len) {
+  x = (uint64_t)(uintptr_t)A.data + k.ox - k.b0;
+  len = k.oy - k.ox;
+}
+
+template <int CH>
+__device__ __forceinline__ void seg_xlen(const BatchArgs &A, const SegChunk32 &k, uint32_t lane,
+                                         uint64_t p0, uint32_t &x, uint32_t &len) {
+  const uint32_t h = (uint32_t)((uint64_t)(uintptr_t)A.data + k.s0 - k.b0);  // bytes before the chunk
+  const uint32_t s0 = (uint32_t)k.s0;
+  uint32_t ox;
+  if (A.offsets) {  // back to back: the left neighbour's end
+    const uint32_t l = (uint32_t)__shfl((int)k.ey, (int)(lane ? lane - 1u : 0u), 64);
+    ox = lane ? l : s0;
+  } else {  // lanes past the batch sit at the chunk end (ey)
+    const bool own = lane < (uint32_t)CH && p0 + lane < A.n;
+    ox = own ? (uint32_t)((p0 + lane) * A.stride) : k.ey;
+  }
+  x = ox - s0 + h;
+  len = k.ey - ox;
+}
+
 // Loads of tile t (bytes [t*T, t*T + T) past b0) of a chunk ending xe past
 // b0. One call site with selected arguments and a compile-time load policy:
 // no load sits in a branch, so the next tile's loads stay in flight while the
@@ -1604,7 +1679,7 @@ constexpr int kSegPlain = 0, kSegTx = 1, kSegRx = 2, kSegDg = 3;
 // (the DG kind asks for at least 3 waves per SIMD, which it would otherwise
 // miss by a few VGPRs; the other kinds are left alone)
 template <int U, int NT, int K, int CH = 64>
-__global__ __launch_bounds__(256, K == kSegTx || K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
+__global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   constexpr bool DG = K == kSegDg;
   constexpr bool RX = K == kSegRx || DG;  // parses each packet's IPv4 header
   constexpr bool tx = K == kSegTx;
@@ -1648,7 +1723,8 @@ __global__ __launch_bounds__(256, K == kSegTx || K == kSegDg ? 3 : 1) void k_seg
 
   uint64_t ch = wave;
   if (wave >= nwave || ch * CH >= A.n) return;
-  SegChunk cur, nxt;
+  using Chunk = typename std::conditional<K == kSegTx, SegChunk32, SegChunk>::type;
+  Chunk cur, nxt;
   seg_load<CH, !RX>(A, sp, ch * CH, lane, cur);
   seg_load<CH, !RX>(A, sp, (ch + nwave) * CH, lane, nxt);
   seg_geom(data, A.n, ch * CH, cur, wbk);
@@ -1674,10 +1750,13 @@ __global__ __launch_bounds__(256, K == kSegTx || K == kSegDg ? 3 : 1) void k_seg
   uint32_t fk = 0, fsum = 0;
   bool exact = false;
   uint32_t carry_l = 0, carry_t = 0;
-  auto begin_chunk = [&](const SegChunk &k) __attribute__((always_inline)) {
-    const Pos x = (Pos)(data + k.ox - k.b0);
-    const Pos y = (Pos)(data + k.oy - k.b0);
-    const uint64_t len = k.oy - k.ox;
+  typename std::conditional<K == kSegTx, uint32_t, uint64_t>::type plen = 0;  // this lane's packet length
+  auto begin_chunk = [&](const Chunk &k, uint64_t p0) __attribute__((always_inline)) {
+    typename std::conditional<K == kSegTx, uint32_t, uint64_t>::type x64, len;
+    seg_xlen<CH>(A, k, lane, p0, x64, len);
+    plen = len;
+    const Pos x = (Pos)x64;
+    const Pos y = x + (Pos)len;
     pt[0].x = x;
     // ragged packets lie back to back: P(end) is the next lane's P(start), so
     // only lane 63 evaluates an end point (the chunk end); RX needs none
@@ -1705,7 +1784,7 @@ __global__ __launch_bounds__(256, K == kSegTx || K == kSegDg ? 3 : 1) void k_seg
     exact = K == kSegPlain && mode == YU_MODE_RAW && __any((int)(len > kLEMax));
     carry_l = carry_t = 0u;
   };
-  begin_chunk(cur);
+  begin_chunk(cur, ch * CH);
 
   uint64_t t = 0;
   // One tile: issue the loads of the next item into cn, then sum c.
@@ -1714,7 +1793,7 @@ __global__ __launch_bounds__(256, K == kSegTx || K == kSegDg ? 3 : 1) void k_seg
     // the chunk's tiles cover [0, xe); a point at a tile's end (xe itself,
     // when tile-aligned) takes the running sums after that tile
     const bool last = t * T + T >= cur.xe;  // wave-uniform
-    SegChunk nn;  // the chunk after next: its loads go out before this
+    Chunk nn;  // the chunk after next: its loads go out before this
                   // step's tile loads, so waiting on them never waits on those
     if (last) {
       seg_geom(data, A.n, (ch + nwave) * CH, nxt, wbk);
@@ -1723,289 +1802,352 @@ __global__ __launch_bounds__(256, K == kSegTx || K == kSegDg ? 3 : 1) void k_seg
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
                           end, cn);
 
-    // chunk sums, address-ordered exclusive prefixes (DPP scan per u)
-    const Pos tb = (Pos)(t * T);
-    // chunk prefix; HP: also the chunk's first half's sum (half-chunk prefixes)
-    uint32_t pl[U], ph[U], ptt[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      ph[u] = sad(c[u].y, sad(c[u].x, 0u));
-      const uint32_t s = sad(c[u].w, sad(c[u].z, ph[u]));
-      const uint32_t inc = group_total<64>(s);
-      pl[u] = carry_l + inc - s;
-      carry_l += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-    }
-    if (exact) {
+    if (K == kSegRx && t == 0u && cur.xe + 24u <= T) {  // wave-uniform
+      // RX on a chunk that lies in one tile with room for every header window
+      // (small received datagrams, bench config 7): straight-line code. No
+      // running carry, no point left for a later tile, each header read whole
+      // from the tile, and a datagram that fills its packet (TotalLength() ==
+      // len) ends where the next lane's starts (a point of its own for lane 63:
+      // the tile's total would count the bytes loaded past the chunk end).
+      // Same checks and result bits as below.
+      uint32_t carry = 0u;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        uint32_t s = __builtin_amdgcn_sad_u8(c[u].x, 0u, 0u);
-        s = __builtin_amdgcn_sad_u8(c[u].y, 0u, s);
-        s = __builtin_amdgcn_sad_u8(c[u].z, 0u, s);
-        s = __builtin_amdgcn_sad_u8(c[u].w, 0u, s);
+        const uint32_t h0 = sad(c[u].y, sad(c[u].x, 0u));
+        const uint32_t s = sad(c[u].w, sad(c[u].z, h0));
         const uint32_t inc = group_total<64>(s);
-        ptt[u] = carry_t + inc - s;
-        carry_t += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-      }
-    }
-    bool here = false;
-#pragma unroll
-    for (int i = 0; i < NP; ++i)
-      if (!(RX && i == 1)) here |= pt[i].x - tb < T;  // (RX and DG have no end point)
-    if (FB) here |= fx - tb < T;
-    if (RX) {  // a header window [floor4(start), +24) still being gathered
-      const Pos hs = pt[0].x & ~(Pos)3;
-      here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
-    }
-    const bool park = __any((int)here);
-    if (park) {  // a packet boundary (or header) lies in this tile
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
+        const uint32_t pl = carry + inc - s;
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         s_data[wid][u * 64 + lane] = c[u];
-        if (HP)
-          ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl[u], pl[u] + ph[u]);
-        else
-          s_pre[wid][u * 64 + lane] = pl[u];
+        ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl, pl + h0);
       }
       __builtin_amdgcn_wave_barrier();
-      bool parsed = false;
-      if (RX && rx.need) {  // gather header dwords held by this tile, parse
-        const Pos q0 = (pt[0].x & ~(Pos)3) - tb;
-        if (q0 <= (Pos)(T - 24u)) {
-          // the whole 24-byte window lies in this tile (q0 wraps past T when
-          // the window began in an earlier one): six reads, no bookkeeping
-          const uint32_t d = (uint32_t)q0 >> 2;
+      const uint32_t *pre2 = s_pre[wid];
+      const uint2 *half = (const uint2 *)s_data[wid];
+      const uint32_t x = (uint32_t)pt[0].x;
+      const uint32_t len = (uint32_t)plen;
+      const uint32_t p0 = seg_point<false>(pre2, half, x);
+      const uint32_t pn = (uint32_t)__shfl((int)p0, (int)(lane < 63u ? lane + 1u : 63u), 64);  // P(next start)
+      uint32_t r = YU_RX_INVALID;
+      if (len >= 20u) {  // IsValid's minimum size
+        const uint32_t d = (x & ~3u) >> 2;
 #pragma unroll
-          for (int j = 0; j < 6; ++j) rx.h[j] = s_dw[d + (uint32_t)j];
-          rx.need = 0u;
-        } else {  // a window across two tiles: the dwords this one holds
-#pragma unroll
-          for (int j = 0; j < 6; ++j) {
-            const Pos q = q0 + 4u * (uint32_t)j;
-            if (((rx.need >> j) & 1u) && q < T) {
-              rx.h[j] = s_dw[(uint32_t)q >> 2];
-              rx.need &= ~(1u << j);
-            }
-          }
-        }
-        if (rx.need == 0u) {
-          uint32_t hl, tl;
-          rx_parse(rx, (uint32_t)pt[0].x & 3u, cur.oy - cur.ox, hl, tl);
-          // a well-formed datagram fills its packet: in a ragged chunk its
-          // transport end is the next lane's start (the marker lane's, for the
-          // chunk's last packet), already evaluated; when every lane's is, the
-          // wave skips the transport-end slot altogether
-          rx.tnext = contig && kMarker && tl == (uint32_t)(cur.oy - cur.ox) ? 1u : 0u;
-          if (DG) {
-            // in contract HeaderLength() >= 20: every point lies at or past
-            // byte 20, so never in a tile that has gone by
-            const uint32_t fo = dg_parse(rx, (uint32_t)pt[0].x & 3u, hl, tl);
-            if (rx.hl) {
-              pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
-              pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
-            }
-            if (fo) {
-              fx = pt[0].x + fo;
-              fk = 2u;
-            }
-          } else {
-            pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
-            pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
-          }
-          parsed = true;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const Pos q = pt[i].x - tb;
-        if (!(RX && i == 1) && q < T) {
-          if (HP) {
-            pt[i].p = seg_point<false>(s_pre[wid], (const uint2 *)s_data[wid], (uint32_t)q);
-          } else {
-            const uint32_t k = (uint32_t)q >> 4;
-            pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
-          }
-        }
-      }
-      if (FB) {  // the field's bytes, weighted by address parity
-        const Pos q = fx - tb;
-        if (q < T) {
-          const uint8_t *sb = (const uint8_t *)s_data[wid];
-          const uint32_t b = sb[q];
-          fsum += (q & 1u) ? b << 8 : b;
-          if (fk == 2u && q + 1u < T) {
-            const uint32_t b1 = sb[q + 1u];
-            fsum += (q & 1u) ? b1 : b1 << 8;
-          }
-          const bool split = fk == 2u && q + 1u == T;  // the field's second byte opens the next tile
-          fk = split ? 1u : 0u;
-          fx = split ? fx + 1u : kNoPt;
-        }
-      }
-      if (RX && !DG && parsed) {
-        // A header straddling two tiles is parsed in the second, but a header
-        // or total length under 20 bytes (IsValid accepts IHL 0..4) can put
-        // its point in the first, whose bytes have gone by. Such a point lies
-        // inside the gathered 24-byte window: P(point) = P(start) + the LE sum
-        // of the window bytes in between, taken from the registers.
-        const uint32_t sh = (uint32_t)pt[0].x & 3u;
-#pragma unroll
-        for (int i = 2; i < 4; ++i) {
-          if (pt[i].x < tb) {
-            const uint32_t b = sh + (uint32_t)(pt[i].x - pt[0].x);  // < sh + 20
-            uint32_t s = pt[0].p;
-#pragma unroll
-            for (int j = 0; j < 6; ++j)
-              s = sad(rx.h[j] & byte_range_mask(4u * (uint32_t)j, sh, b), s);
-            pt[i].p = s;
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (exact) {  // second pass, same buffer: the byte-sum prefixes
-#pragma unroll
-        for (int u = 0; u < U; ++u) s_pre[wid][u * 64 + lane] = ptt[u];
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int i = 0; i < NP; ++i) {
-          const Pos q = pt[i].x - tb;
-          if (q < T) {
-            const uint32_t k = (uint32_t)q >> 4;
-            pt[i].t = s_pre[wid][k] + seg_part<true>(s_data[wid][k], (uint32_t)q & 15u);
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NP; ++i)
-      if (!(RX && i == 1) && pt[i].x - tb == T) pt[i].p = carry_l;
-    if (exact) {
-#pragma unroll
-      for (int i = 0; i < NP; ++i)
-        if (pt[i].x - tb == T) pt[i].t = carry_t;
-    }
-
-    if (!last) {
-      ++t;
-      return false;
-    }
-    // end sums: the next lane's start (ragged), else this lane's end point
-    const int nl = (int)(lane < 63u ? lane + 1u : 63u);
-    const uint32_t nx_p = (uint32_t)__shfl((int)pt[0].p, nl, 64);
-    const uint32_t nx_t = (uint32_t)__shfl((int)pt[0].t, nl, 64);
-    const bool own_end = !contig || (!kMarker && lane == 63u);
-    const uint32_t p3 = RX && rx.tnext ? nx_p : pt[3].p;  // P(transport end)
-    const uint32_t pe = own_end ? pt[1].p : nx_p;
-    const uint32_t te = own_end ? pt[1].t : nx_t;
-    const uint64_t p = ch * CH + lane;
-    // TX in place (wbk): this lane's field offset in the tile (wf: it has one),
-    // its line when stored whole (64: not), its value
-    Pos wq = 0;
-    bool wf = false;
-    uint32_t wl = 64u, wr = 0u;
-    const Pos x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);  // the chunk's start (wbk: 32-bit)
-    if (lane < (uint32_t)CH && p < A.n) {
-      const uint32_t odd = (uint32_t)pt[0].x & 1u;
-      if (DG) {
-        // IPv4 header field: ^Checksum(b[:HeaderLength()]) with the field as 0
-        // (network/ipv4/ipv4.go:85-94); transport field: the sender's value
-        // over b[HeaderLength():TotalLength()] with its field as 0 and the
-        // pseudo header + length from the datagram (sendUDP / sendTCP /
-        // sendICMPv4, see include/yucsum.h)
-        uint32_t ip = 0u, l4 = 0u;
-        const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
-        if (rx.hl) ip = ~fold32(le_to_be(p2 - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
-        if (rx.fo) l4 = ~fold32(le_to_be(p3 - p2 - fsum, odd) + rx.pseudo) & 0xFFFFu;
-        if (A.out) {  // out[2p], out[2p + 1]: one 32-bit store when aligned
-          if (((uintptr_t)A.out & 3u) == 0u) {
-            ((uint32_t *)A.out)[p] = ip | (l4 << 16);
-          } else {
-            A.out[2u * p] = (uint16_t)ip;
-            A.out[2u * p + 1u] = (uint16_t)l4;
-          }
-        }
-        if (A.fill) {
-          if (rx.hl) put_be16(A.fill + cur.ox + 10u, ip);
-          if (rx.fo) put_be16(A.fill + cur.ox + rx.fo, l4);
-        }
-      } else if (RX) {
-        // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
-        // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
-        uint32_t r = rx.flags;
+        for (int j = 0; j < 6; ++j) rx.h[j] = s_dw[d + (uint32_t)j];
+        uint32_t hl, tl;
+        rx_parse(rx, x & 3u, len, hl, tl);
+        r = rx.flags;
         if (!(r & YU_RX_INVALID)) {
-          const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
-          const uint32_t ip = fold32(le_to_be(p2 - pt[0].p, odd));
+          // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
+          // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
+          const uint32_t odd = x & 1u;
+          const uint32_t p2 = rx.h20 ? p0 + rx.hsum : seg_point<false>(pre2, half, x + hl);
+          const uint32_t ip = fold32(le_to_be(p2 - p0, odd));
           if (ip == 0u || ip == 0xFFFFu) r |= YU_RX_IP_OK;
           if (r & YU_RX_L4) {
+            const uint32_t p3 = tl == len && lane < 63u ? pn : seg_point<false>(pre2, half, x + tl);
             const uint32_t l4 = fold32(le_to_be(p3 - p2, odd) + rx.pseudo);
             if (l4 == 0u || l4 == 0xFFFFu) r |= YU_RX_L4_OK;
           }
         }
-        if (A.out) A.out[p] = (uint16_t)r;
-      } else {
-        uint32_t v;
-        if (exact) {
-          const uint32_t L = pe - pt[0].p;
-          const uint32_t S = te - pt[0].t;
-          const uint32_t b = (L - S) * kInv255;  // odd-address bytes
-          const uint32_t a = S - b;              // even-address bytes
-          v = odd ? a + (b << 8) : (a << 8) + b;
-        } else {
-          v = le_to_be(pe - pt[0].p - (tx ? fsum : 0u), odd);
+      }
+      const uint64_t p = ch * CH + lane;
+      if (lane < (uint32_t)CH && p < A.n && A.out) A.out[p] = (uint16_t)r;
+    } else {
+
+      const Pos tb = (Pos)(t * T);
+      bool here = false;  // a packet boundary (or header) lies in this tile
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+        if (!(RX && i == 1)) here |= pt[i].x - tb < T;  // (RX and DG have no end point)
+      if (FB) here |= fx - tb < T;
+      if (RX) {  // a header window [floor4(start), +24) still being gathered
+        const Pos hs = pt[0].x & ~(Pos)3;
+        here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
+      }
+      const bool park = __any((int)here);
+      // chunk sums, address-ordered exclusive prefixes (DPP scan per u). The TX
+      // kind parks each column as its scan completes (FUSE: no prefix array
+      // live across the scan, registers its in-place write-back needs); the
+      // others after the scan
+      constexpr bool FUSE = K == kSegTx;
+      // chunk prefix; HP: also the chunk's first half's sum (half-chunk prefixes)
+      uint32_t pl[U], ph[U], ptt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ph[u] = sad(c[u].y, sad(c[u].x, 0u));
+        const uint32_t s = sad(c[u].w, sad(c[u].z, ph[u]));
+        const uint32_t inc = group_total<64>(s);
+        pl[u] = carry_l + inc - s;
+        carry_l += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        if (FUSE && park) {
+          s_data[wid][u * 64 + lane] = c[u];
+          ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl[u], pl[u] + ph[u]);
         }
-        const uint64_t len = cur.oy - cur.ox;
-        uint8_t *pk = A.fill ? A.fill + cur.ox : nullptr;
-        if (tx && wbk && park && fld + 2u <= len) {
-          // the field's offset in the parked (last) tile, wrapping below it;
-          // its line is stored whole below when the field lies in one line of
-          // this tile that holds no byte outside this chunk
-          wq = pt[0].x + fld - tb;
-          wf = true;
-          const Pos ls = wq & ~(Pos)127;
-          // (wq wraps for a field in an earlier tile: wq <= T - 2 keeps those out,
-          // a field ending right at this tile's start included)
-          if (wq <= T - 2u && (wq & 127u) != 127u && tb + ls >= x0 && tb + ls + 128u <= cur.xe) {
-            wl = (uint32_t)wq >> 7;
-            pk = nullptr;  // no 2-byte store
+      }
+      if (exact) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          uint32_t s = __builtin_amdgcn_sad_u8(c[u].x, 0u, 0u);
+          s = __builtin_amdgcn_sad_u8(c[u].y, 0u, s);
+          s = __builtin_amdgcn_sad_u8(c[u].z, 0u, s);
+          s = __builtin_amdgcn_sad_u8(c[u].w, 0u, s);
+          const uint32_t inc = group_total<64>(s);
+          ptt[u] = carry_t + inc - s;
+          carry_t += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        }
+      }
+      if (park) {
+        if (!FUSE) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            s_data[wid][u * 64 + lane] = c[u];
+            if (HP)
+              ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl[u], pl[u] + ph[u]);
+            else
+              s_pre[wid][u * 64 + lane] = pl[u];
           }
         }
-        const uint32_t r = packet_value(A, v, len, cur.sd);
-        if (A.out) A.out[p] = (uint16_t)r;
-        wr = r;
-        if (pk) store_field(A, r, pk, (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
+        __builtin_amdgcn_wave_barrier();
+        bool parsed = false;
+        if (RX && rx.need) {  // gather header dwords held by this tile, parse
+          const Pos q0 = (pt[0].x & ~(Pos)3) - tb;
+          if (q0 <= (Pos)(T - 24u)) {
+            // the whole 24-byte window lies in this tile (q0 wraps past T when
+            // the window began in an earlier one): six reads, no bookkeeping
+            const uint32_t d = (uint32_t)q0 >> 2;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) rx.h[j] = s_dw[d + (uint32_t)j];
+            rx.need = 0u;
+          } else {  // a window across two tiles: the dwords this one holds
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+              const Pos q = q0 + 4u * (uint32_t)j;
+              if (((rx.need >> j) & 1u) && q < T) {
+                rx.h[j] = s_dw[(uint32_t)q >> 2];
+                rx.need &= ~(1u << j);
+              }
+            }
+          }
+          if (rx.need == 0u) {
+            uint32_t hl, tl;
+            rx_parse(rx, (uint32_t)pt[0].x & 3u, plen, hl, tl);
+            // a well-formed datagram fills its packet: in a ragged chunk its
+            // transport end is the next lane's start (the marker lane's, for the
+            // chunk's last packet), already evaluated; when every lane's is, the
+            // wave skips the transport-end slot altogether
+            rx.tnext = contig && kMarker && tl == (uint32_t)plen ? 1u : 0u;
+            if (DG) {
+              // in contract HeaderLength() >= 20: every point lies at or past
+              // byte 20, so never in a tile that has gone by
+              const uint32_t fo = dg_parse(rx, (uint32_t)pt[0].x & 3u, hl, tl);
+              if (rx.hl) {
+                pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
+                pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
+              }
+              if (fo) {
+                fx = pt[0].x + fo;
+                fk = 2u;
+              }
+            } else {
+              pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
+              pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
+            }
+            parsed = true;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const Pos q = pt[i].x - tb;
+          if (!(RX && i == 1) && q < T) {
+            if (HP) {
+              pt[i].p = seg_point<false>(s_pre[wid], (const uint2 *)s_data[wid], (uint32_t)q);
+            } else {
+              const uint32_t k = (uint32_t)q >> 4;
+              pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
+            }
+          }
+        }
+        if (FB) {  // the field's bytes, weighted by address parity
+          const Pos q = fx - tb;
+          if (q < T) {
+            const uint8_t *sb = (const uint8_t *)s_data[wid];
+            const uint32_t b = sb[q];
+            fsum += (q & 1u) ? b << 8 : b;
+            if (fk == 2u && q + 1u < T) {
+              const uint32_t b1 = sb[q + 1u];
+              fsum += (q & 1u) ? b1 : b1 << 8;
+            }
+            const bool split = fk == 2u && q + 1u == T;  // the field's second byte opens the next tile
+            fk = split ? 1u : 0u;
+            fx = split ? fx + 1u : kNoPt;
+          }
+        }
+        if (RX && !DG && parsed) {
+          // A header straddling two tiles is parsed in the second, but a header
+          // or total length under 20 bytes (IsValid accepts IHL 0..4) can put
+          // its point in the first, whose bytes have gone by. Such a point lies
+          // inside the gathered 24-byte window: P(point) = P(start) + the LE sum
+          // of the window bytes in between, taken from the registers.
+          const uint32_t sh = (uint32_t)pt[0].x & 3u;
+#pragma unroll
+          for (int i = 2; i < 4; ++i) {
+            if (pt[i].x < tb) {
+              const uint32_t b = sh + (uint32_t)(pt[i].x - pt[0].x);  // < sh + 20
+              uint32_t s = pt[0].p;
+#pragma unroll
+              for (int j = 0; j < 6; ++j)
+                s = sad(rx.h[j] & byte_range_mask(4u * (uint32_t)j, sh, b), s);
+              pt[i].p = s;
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (exact) {  // second pass, same buffer: the byte-sum prefixes
+#pragma unroll
+          for (int u = 0; u < U; ++u) s_pre[wid][u * 64 + lane] = ptt[u];
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int i = 0; i < NP; ++i) {
+            const Pos q = pt[i].x - tb;
+            if (q < T) {
+              const uint32_t k = (uint32_t)q >> 4;
+              pt[i].t = s_pre[wid][k] + seg_part<true>(s_data[wid][k], (uint32_t)q & 15u);
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
       }
-    }
-    if (tx && wbk && park) {  // wave-uniform: the in-place write-back
-      // 1. Every field byte that lies in the tile goes into its parked copy, the
-      //    ones left to their 2-byte stores too (same bytes: a line stored whole
-      //    that holds one stays right).
-      uint8_t *sb = (uint8_t *)s_data[wid];
-      if (wf && wq < T) sb[wq] = (uint8_t)(wr >> 8);
-      if (wf && wq + 1u < T) sb[wq + 1u] = (uint8_t)wr;  // (wq + 1 == 0: a field from the tile before)
-      // 2. The lines holding a field of their own, as a 64-bit mask (T / 128 <= 64 lines).
-      const uint64_t m = (uint64_t)wave_or(wl < 32u ? 1u << wl : 0u) |
-                         ((uint64_t)wave_or(wl >= 32u && wl < 64u ? 1u << (wl - 32u) : 0u) << 32);
-      wave_lds_fence();
-      // 3. Those lines from the tile copy, as full-line 16-byte stores (8 lanes
-      //    per line, one contiguous KiB per instruction), non-temporal. Memory
-      //    then sees whole lines, not one partial write per field.
-      const __amdgpu_buffer_rsrc_t wr_r = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)(A.fill + (cur.b0 + tb - data)), (short)0, (int)T, 0x00020000);
-      // (one 16-byte LDS read in flight per store: the next tile's loads hold
-      // 32 VGPRs here, and the TX kind must stay within 168)
-#pragma unroll 1
-      for (int u = 0; u < U; ++u) {
-        const uint32_t k = (uint32_t)u * 64u + lane;
-        const uint4 d = s_data[wid][k];
-        const uint32_t off = ((m >> (k >> 3)) & 1u) ? 16u * k : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 2);  // nt
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+        if (!(RX && i == 1) && pt[i].x - tb == T) pt[i].p = carry_l;
+      if (exact) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+          if (pt[i].x - tb == T) pt[i].t = carry_t;
+      }
+
+      if (!last) {
+        ++t;
+        return false;
+      }
+      // end sums: the next lane's start (ragged), else this lane's end point
+      const int nl = (int)(lane < 63u ? lane + 1u : 63u);
+      const uint32_t nx_p = (uint32_t)__shfl((int)pt[0].p, nl, 64);
+      const uint32_t nx_t = (uint32_t)__shfl((int)pt[0].t, nl, 64);
+      const bool own_end = !contig || (!kMarker && lane == 63u);
+      const uint32_t p3 = RX && rx.tnext ? nx_p : pt[3].p;  // P(transport end)
+      const uint32_t pe = own_end ? pt[1].p : nx_p;
+      const uint32_t te = own_end ? pt[1].t : nx_t;
+      const uint64_t p = ch * CH + lane;
+      // TX in place (wbk): this lane's field offset in the tile (wf: it has one),
+      // its line when stored whole (64: not), its value
+      Pos wq = 0;
+      bool wf = false;
+      uint32_t wl = 64u, wr = 0u;
+      Pos x0 = 0;  // the chunk's start (wbk: the TX kind, 32-bit)
+      if (wbk) x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);
+      if (lane < (uint32_t)CH && p < A.n) {
+        const uint32_t odd = (uint32_t)pt[0].x & 1u;
+        if (DG) {
+          // IPv4 header field: ^Checksum(b[:HeaderLength()]) with the field as 0
+          // (network/ipv4/ipv4.go:85-94); transport field: the sender's value
+          // over b[HeaderLength():TotalLength()] with its field as 0 and the
+          // pseudo header + length from the datagram (sendUDP / sendTCP /
+          // sendICMPv4, see include/yucsum.h)
+          uint32_t ip = 0u, l4 = 0u;
+          const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
+          if (rx.hl) ip = ~fold32(le_to_be(p2 - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
+          if (rx.fo) l4 = ~fold32(le_to_be(p3 - p2 - fsum, odd) + rx.pseudo) & 0xFFFFu;
+          if (A.out) {  // out[2p], out[2p + 1]: one 32-bit store when aligned
+            if (((uintptr_t)A.out & 3u) == 0u) {
+              ((uint32_t *)A.out)[p] = ip | (l4 << 16);
+            } else {
+              A.out[2u * p] = (uint16_t)ip;
+              A.out[2u * p + 1u] = (uint16_t)l4;
+            }
+          }
+          if (A.fill) {
+            uint8_t *pk = A.fill + (cur.b0 + pt[0].x - data);
+            if (rx.hl) put_be16(pk + 10u, ip);
+            if (rx.fo) put_be16(pk + rx.fo, l4);
+          }
+        } else if (RX) {
+          // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
+          // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
+          uint32_t r = rx.flags;
+          if (!(r & YU_RX_INVALID)) {
+            const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
+            const uint32_t ip = fold32(le_to_be(p2 - pt[0].p, odd));
+            if (ip == 0u || ip == 0xFFFFu) r |= YU_RX_IP_OK;
+            if (r & YU_RX_L4) {
+              const uint32_t l4 = fold32(le_to_be(p3 - p2, odd) + rx.pseudo);
+              if (l4 == 0u || l4 == 0xFFFFu) r |= YU_RX_L4_OK;
+            }
+          }
+          if (A.out) A.out[p] = (uint16_t)r;
+        } else {
+          uint32_t v;
+          if (exact) {
+            const uint32_t L = pe - pt[0].p;
+            const uint32_t S = te - pt[0].t;
+            const uint32_t b = (L - S) * kInv255;  // odd-address bytes
+            const uint32_t a = S - b;              // even-address bytes
+            v = odd ? a + (b << 8) : (a << 8) + b;
+          } else {
+            v = le_to_be(pe - pt[0].p - (tx ? fsum : 0u), odd);
+          }
+          const uint64_t len = plen;
+          uint8_t *pk = A.fill ? A.fill + (cur.b0 + pt[0].x - data) : nullptr;
+          if (tx && wbk && park && fld + 2u <= len) {
+            // the field's offset in the parked (last) tile, wrapping below it;
+            // its line is stored whole below when the field lies in one line of
+            // this tile that holds no byte outside this chunk
+            wq = pt[0].x + fld - tb;
+            wf = true;
+            const Pos ls = wq & ~(Pos)127;
+            // (wq wraps for a field in an earlier tile: wq <= T - 2 keeps those out,
+            // a field ending right at this tile's start included)
+            if (wq <= T - 2u && (wq & 127u) != 127u && tb + ls >= x0 && tb + ls + 128u <= cur.xe) {
+              wl = (uint32_t)wq >> 7;
+              pk = nullptr;  // no 2-byte store
+            }
+          }
+          const uint32_t r = packet_value(A, v, len, cur.sd);
+          if (A.out) A.out[p] = (uint16_t)r;
+          wr = r;
+          if (pk) store_field(A, r, pk, (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
+        }
+      }
+      if (tx && wbk && park) {  // wave-uniform: the in-place write-back
+        // 1. Every field byte that lies in the tile goes into its parked copy, the
+        //    ones left to their 2-byte stores too (same bytes: a line stored whole
+        //    that holds one stays right).
+        uint8_t *sb = (uint8_t *)s_data[wid];
+        if (wf && wq < T) sb[wq] = (uint8_t)(wr >> 8);
+        if (wf && wq + 1u < T) sb[wq + 1u] = (uint8_t)wr;  // (wq + 1 == 0: a field from the tile before)
+        // 2. The lines holding a field of their own, as a 64-bit mask (T / 128 <= 64 lines).
+        const uint64_t m = (uint64_t)wave_or(wl < 32u ? 1u << wl : 0u) |
+                           ((uint64_t)wave_or(wl >= 32u && wl < 64u ? 1u << (wl - 32u) : 0u) << 32);
+        wave_lds_fence();
+        // 3. Those lines from the tile copy, as full-line 16-byte stores (8 lanes
+        //    per line, one contiguous KiB per instruction), non-temporal. Memory
+        //    then sees whole lines, not one partial write per field.
+        const __amdgpu_buffer_rsrc_t wr_r = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(A.fill + (cur.b0 + tb - data)), (short)0, (int)T, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t k = (uint32_t)u * 64u + lane;
+          const uint4 d = s_data[wid][k];
+          const uint32_t off = ((m >> (k >> 3)) & 1u) ? 16u * k : kOOB;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 2);  // nt
+        }
       }
     }
     if ((ch + nwave) * CH >= A.n) return true;
     cur = nxt;
     nxt = nn;
     ch += nwave;
-    begin_chunk(cur);
+    begin_chunk(cur, ch * CH);
     t = 0;
     return false;
   };
