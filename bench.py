@@ -179,7 +179,7 @@ class Workload:
 
     def kernel_name(self) -> str:
         if self.offsets is not None:
-            return batch.ragged_variant(self.mode, self.n)
+            return batch.ragged_variant(self.mode, self.n, fill=self.fill)
         return batch.variant(self.L, self.L, self.mode, self.data[0].data_ptr() & 15, n=self.n)
 
 

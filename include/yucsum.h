@@ -340,6 +340,9 @@ const char *yu_uniform_variant_n(uint64_t stride, uint32_t len, uint64_t n,
  * packets (bursts of up to 4096 packets take a wave per packet). */
 const char *yu_ragged_variant(int mode);
 const char *yu_ragged_variant_n(int mode, uint64_t n);
+/* The kernel variant yu_csum_fill_ragged launches for a batch of n packets (the
+ * TX modes write in place through their own k_seg form). */
+const char *yu_ragged_fill_variant_n(int mode, uint64_t n);
 
 #ifdef __cplusplus
 }

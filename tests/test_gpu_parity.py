@@ -368,6 +368,7 @@ def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, shift):
         blob[offs[:-1].astype(np.int64) + 12] = 0x50
     addrs = _rand(rng, 8 * npk)
     want = oracle_c.batch(blob, mode, offsets=offs, addrs=addrs if mode != O.MODE_ICMP else None)
+    assert batch.ragged_variant(mode, npk, fill=True) == ("k_seg<8,txw,c16>" if npk < 65536 else "k_seg<8,txw>")
     pre = _rand(rng, shift)
     whole = _to(dev, np.concatenate([pre, blob]))
     d = whole[shift:]

@@ -1,10 +1,10 @@
-# round 4, call D: k_seg with the RX kind's one-tile straight-line path, the TX kind
+# round 4, call E: k_seg with the in-place TXW kind (whole-line write-back) and the
 # on 32-bit chunk loads with the park fused into its scan (and the whole-line
-# in-place write-back): GPU suite, fill tests with the write-back off, kbench A/B
+# the write-back off, kbench A/B
 # against the round-start library (tools/old), the driver-style bench line
 set -o pipefail
 mkdir -p gpurun_out
-T=r04d
+T=r04e
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1 || { tail -60 gpurun_out/gpu_tests_$T.log; exit 1; }
 tail -1 gpurun_out/gpu_tests_$T.log
 YU_FILL_WB=0 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "fill or fuzz or kernel_verified" --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_${T}_wb0.log 2>&1 || { tail -40 gpurun_out/gpu_tests_${T}_wb0.log; exit 1; }
@@ -16,4 +16,5 @@ timeout -k 10 900 bash tools/ab.sh "16 $O" "16" "16 $O" "16" "16 $O" "16" "8 $O"
 grep -E "^==|round 2" gpurun_out/kbench_ab_$T.log
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || { tail gpurun_out/bench_$T.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/bench_$T.json'));print(d['value'],d['roofline']['frac']);[print(k,v['kernel_avg_us'],v['roofline_frac']) for k,v in d['other_configs'].items()]"
+CFGS="12 13" timeout -k 10 600 bash tools/profile.sh $T || exit 1
 echo ok

@@ -22,7 +22,7 @@ EXPORTS = (
     "yu_csum_batch_host_iov_multi",
     "yu_csum_fill_host_uniform", "yu_csum_fill_host_ragged", "yu_csum_fill_host_iov",
     "yu_abi_version", "yu_strerror", "yu_device_count", "yu_uniform_variant", "yu_uniform_variant_n",
-    "yu_ragged_variant", "yu_ragged_variant_n",
+    "yu_ragged_variant", "yu_ragged_variant_n", "yu_ragged_fill_variant_n",
 )
 
 YU_OK, YU_EINVAL, YU_ENODEV, YU_ENOMEM, YU_EHIP_BASE = 0, -22, -19, -12, -1000
@@ -100,6 +100,8 @@ def lib() -> ctypes.CDLL:
     L.yu_ragged_variant.argtypes = [i32]
     L.yu_ragged_variant_n.restype = c.c_char_p
     L.yu_ragged_variant_n.argtypes = [i32, u64]
+    L.yu_ragged_fill_variant_n.restype = c.c_char_p
+    L.yu_ragged_fill_variant_n.argtypes = [i32, u64]
     del u8
     _lib = L
     return L

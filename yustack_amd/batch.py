@@ -315,10 +315,12 @@ def rx_accepted(flags: torch.Tensor) -> torch.Tensor:
     return ok_ip & ok_l4
 
 
-def ragged_variant(mode="raw", n: int = 1 << 20) -> str:
+def ragged_variant(mode="raw", n: int = 1 << 20, fill: bool = False) -> str:
     """Name of the kernel the ragged path launches for this mode and batch size
-    (bursts of up to 4096 packets take a wave per packet)."""
-    return lib().yu_ragged_variant_n(_mode(mode), n).decode()
+    (bursts of up to 4096 packets take a wave per packet); ``fill``: the in-place
+    form (yu_csum_fill_ragged)."""
+    f = lib().yu_ragged_fill_variant_n if fill else lib().yu_ragged_variant_n
+    return f(_mode(mode), n).decode()
 
 
 def variant(stride: int, length: int, mode="raw", align16: int = 0, n: int = 2) -> str:

@@ -1675,6 +1675,11 @@ __device__ __forceinline__ uint64_t seg_waves(const BatchArgs &A) {
 // RX's points; the IPv4 field comes off the parsed header's registers and
 // the transport field's two bytes are read from the tile that holds them).
 constexpr int kSegPlain = 0, kSegTx = 1, kSegRx = 2, kSegDg = 3;
+// TXW: the TX kind writing ragged batches in place with the whole-line write-back
+// (32-bit chunk loads, the park fused into the scan: the registers the
+// write-back needs; TX itself keeps the layout that serves its result-array
+// form best, 26.1 vs 26.8 us on kbench 8)
+constexpr int kSegTxW = 4;
 
 // (the DG kind asks for at least 3 waves per SIMD, which it would otherwise
 // miss by a few VGPRs; the other kinds are left alone)
@@ -1682,7 +1687,8 @@ template <int U, int NT, int K, int CH = 64>
 __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   constexpr bool DG = K == kSegDg;
   constexpr bool RX = K == kSegRx || DG;  // parses each packet's IPv4 header
-  constexpr bool tx = K == kSegTx;
+  constexpr bool TXW = K == kSegTxW;
+  constexpr bool tx = K == kSegTx || TXW;
   constexpr bool FB = tx || DG;                 // a field whose bytes are read from the tile
   constexpr int NP = K == kSegRx || DG ? 4 : 2;  // point slots in use
   constexpr uint32_t T = 64u * 16u * U;
@@ -1702,11 +1708,10 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   const uint64_t end = A.offsets ? data + A.offsets[A.n] : A.end;
   const uint32_t *s_dw = (const uint32_t *)s_data[wid];
   const bool contig = A.offsets != nullptr;  // ragged: packets back to back
-  // TX kind writing in place on a ragged batch: the fields go into the parked
+  // TXW kind (writing a ragged batch in place): the fields go into the parked
   // last tile of each chunk and its whole 128-byte lines are stored back with
-  // non-temporal stores (A.uf != 0; 0 = a 2-byte store per field). See the chunk
-  // epilogue.
-  const bool wbk = tx && A.fill && contig && A.uf != 0u;
+  // non-temporal stores. See the chunk epilogue.
+  const bool wbk = TXW && A.fill && contig;
   // Positions relative to the chunk's b0: 64-bit for the plain kind (RAW packets
   // up to YU_MAX_RAW_LEN), 32-bit for the TX / RX / DG kinds, whose packets are
   // at most 65535 bytes (include/yucsum.h), so a 64-packet chunk spans < 4.2 MB
@@ -1723,7 +1728,7 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
 
   uint64_t ch = wave;
   if (wave >= nwave || ch * CH >= A.n) return;
-  using Chunk = typename std::conditional<K == kSegTx, SegChunk32, SegChunk>::type;
+  using Chunk = typename std::conditional<TXW, SegChunk32, SegChunk>::type;
   Chunk cur, nxt;
   seg_load<CH, !RX>(A, sp, ch * CH, lane, cur);
   seg_load<CH, !RX>(A, sp, (ch + nwave) * CH, lane, nxt);
@@ -1750,9 +1755,9 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   uint32_t fk = 0, fsum = 0;
   bool exact = false;
   uint32_t carry_l = 0, carry_t = 0;
-  typename std::conditional<K == kSegTx, uint32_t, uint64_t>::type plen = 0;  // this lane's packet length
+  typename std::conditional<TXW, uint32_t, uint64_t>::type plen = 0;  // this lane's packet length
   auto begin_chunk = [&](const Chunk &k, uint64_t p0) __attribute__((always_inline)) {
-    typename std::conditional<K == kSegTx, uint32_t, uint64_t>::type x64, len;
+    typename std::conditional<TXW, uint32_t, uint64_t>::type x64, len;
     seg_xlen<CH>(A, k, lane, p0, x64, len);
     plen = len;
     const Pos x = (Pos)x64;
@@ -1802,345 +1807,293 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
                           end, cn);
 
-    if (K == kSegRx && t == 0u && cur.xe + 24u <= T) {  // wave-uniform
-      // RX on a chunk that lies in one tile with room for every header window
-      // (small received datagrams, bench config 7): straight-line code. No
-      // running carry, no point left for a later tile, each header read whole
-      // from the tile, and a datagram that fills its packet (TotalLength() ==
-      // len) ends where the next lane's starts (a point of its own for lane 63:
-      // the tile's total would count the bytes loaded past the chunk end).
-      // Same checks and result bits as below.
-      uint32_t carry = 0u;
+
+    const Pos tb = (Pos)(t * T);
+    bool here = false;  // a packet boundary (or header) lies in this tile
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+      if (!(RX && i == 1)) here |= pt[i].x - tb < T;  // (RX and DG have no end point)
+    if (FB) here |= fx - tb < T;
+    if (RX) {  // a header window [floor4(start), +24) still being gathered
+      const Pos hs = pt[0].x & ~(Pos)3;
+      here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
+    }
+    const bool park = __any((int)here);
+    // chunk sums, address-ordered exclusive prefixes (DPP scan per u). The TX
+    // kind parks each column as its scan completes (FUSE: no prefix array
+    // live across the scan, registers its in-place write-back needs); the
+    // others after the scan
+    constexpr bool FUSE = TXW;
+    // chunk prefix; HP: also the chunk's first half's sum (half-chunk prefixes)
+    uint32_t pl[U], ph[U], ptt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ph[u] = sad(c[u].y, sad(c[u].x, 0u));
+      const uint32_t s = sad(c[u].w, sad(c[u].z, ph[u]));
+      const uint32_t inc = group_total<64>(s);
+      pl[u] = carry_l + inc - s;
+      carry_l += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+      if (FUSE && park) {
+        s_data[wid][u * 64 + lane] = c[u];
+        ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl[u], pl[u] + ph[u]);
+      }
+    }
+    if (exact) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t h0 = sad(c[u].y, sad(c[u].x, 0u));
-        const uint32_t s = sad(c[u].w, sad(c[u].z, h0));
+        uint32_t s = __builtin_amdgcn_sad_u8(c[u].x, 0u, 0u);
+        s = __builtin_amdgcn_sad_u8(c[u].y, 0u, s);
+        s = __builtin_amdgcn_sad_u8(c[u].z, 0u, s);
+        s = __builtin_amdgcn_sad_u8(c[u].w, 0u, s);
         const uint32_t inc = group_total<64>(s);
-        const uint32_t pl = carry + inc - s;
-        carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        s_data[wid][u * 64 + lane] = c[u];
-        ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl, pl + h0);
+        ptt[u] = carry_t + inc - s;
+        carry_t += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+      }
+    }
+    if (park) {
+      if (!FUSE) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          s_data[wid][u * 64 + lane] = c[u];
+          if (HP)
+            ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl[u], pl[u] + ph[u]);
+          else
+            s_pre[wid][u * 64 + lane] = pl[u];
+        }
       }
       __builtin_amdgcn_wave_barrier();
-      const uint32_t *pre2 = s_pre[wid];
-      const uint2 *half = (const uint2 *)s_data[wid];
-      const uint32_t x = (uint32_t)pt[0].x;
-      const uint32_t len = (uint32_t)plen;
-      const uint32_t p0 = seg_point<false>(pre2, half, x);
-      const uint32_t pn = (uint32_t)__shfl((int)p0, (int)(lane < 63u ? lane + 1u : 63u), 64);  // P(next start)
-      uint32_t r = YU_RX_INVALID;
-      if (len >= 20u) {  // IsValid's minimum size
-        const uint32_t d = (x & ~3u) >> 2;
+      bool parsed = false;
+      if (RX && rx.need) {  // gather header dwords held by this tile, parse
+        const Pos q0 = (pt[0].x & ~(Pos)3) - tb;
+        if (q0 <= (Pos)(T - 24u)) {
+          // the whole 24-byte window lies in this tile (q0 wraps past T when
+          // the window began in an earlier one): six reads, no bookkeeping
+          const uint32_t d = (uint32_t)q0 >> 2;
 #pragma unroll
-        for (int j = 0; j < 6; ++j) rx.h[j] = s_dw[d + (uint32_t)j];
-        uint32_t hl, tl;
-        rx_parse(rx, x & 3u, len, hl, tl);
-        r = rx.flags;
+          for (int j = 0; j < 6; ++j) rx.h[j] = s_dw[d + (uint32_t)j];
+          rx.need = 0u;
+        } else {  // a window across two tiles: the dwords this one holds
+#pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            const Pos q = q0 + 4u * (uint32_t)j;
+            if (((rx.need >> j) & 1u) && q < T) {
+              rx.h[j] = s_dw[(uint32_t)q >> 2];
+              rx.need &= ~(1u << j);
+            }
+          }
+        }
+        if (rx.need == 0u) {
+          uint32_t hl, tl;
+          rx_parse(rx, (uint32_t)pt[0].x & 3u, plen, hl, tl);
+          // a well-formed datagram fills its packet: in a ragged chunk its
+          // transport end is the next lane's start (the marker lane's, for the
+          // chunk's last packet), already evaluated; when every lane's is, the
+          // wave skips the transport-end slot altogether
+          rx.tnext = contig && kMarker && tl == (uint32_t)plen ? 1u : 0u;
+          if (DG) {
+            // in contract HeaderLength() >= 20: every point lies at or past
+            // byte 20, so never in a tile that has gone by
+            const uint32_t fo = dg_parse(rx, (uint32_t)pt[0].x & 3u, hl, tl);
+            if (rx.hl) {
+              pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
+              pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
+            }
+            if (fo) {
+              fx = pt[0].x + fo;
+              fk = 2u;
+            }
+          } else {
+            pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
+            pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
+          }
+          parsed = true;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const Pos q = pt[i].x - tb;
+        if (!(RX && i == 1) && q < T) {
+          if (HP) {
+            pt[i].p = seg_point<false>(s_pre[wid], (const uint2 *)s_data[wid], (uint32_t)q);
+          } else {
+            const uint32_t k = (uint32_t)q >> 4;
+            pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
+          }
+        }
+      }
+      if (FB) {  // the field's bytes, weighted by address parity
+        const Pos q = fx - tb;
+        if (q < T) {
+          const uint8_t *sb = (const uint8_t *)s_data[wid];
+          const uint32_t b = sb[q];
+          fsum += (q & 1u) ? b << 8 : b;
+          if (fk == 2u && q + 1u < T) {
+            const uint32_t b1 = sb[q + 1u];
+            fsum += (q & 1u) ? b1 : b1 << 8;
+          }
+          const bool split = fk == 2u && q + 1u == T;  // the field's second byte opens the next tile
+          fk = split ? 1u : 0u;
+          fx = split ? fx + 1u : kNoPt;
+        }
+      }
+      if (RX && !DG && parsed) {
+        // A header straddling two tiles is parsed in the second, but a header
+        // or total length under 20 bytes (IsValid accepts IHL 0..4) can put
+        // its point in the first, whose bytes have gone by. Such a point lies
+        // inside the gathered 24-byte window: P(point) = P(start) + the LE sum
+        // of the window bytes in between, taken from the registers.
+        const uint32_t sh = (uint32_t)pt[0].x & 3u;
+#pragma unroll
+        for (int i = 2; i < 4; ++i) {
+          if (pt[i].x < tb) {
+            const uint32_t b = sh + (uint32_t)(pt[i].x - pt[0].x);  // < sh + 20
+            uint32_t s = pt[0].p;
+#pragma unroll
+            for (int j = 0; j < 6; ++j)
+              s = sad(rx.h[j] & byte_range_mask(4u * (uint32_t)j, sh, b), s);
+            pt[i].p = s;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (exact) {  // second pass, same buffer: the byte-sum prefixes
+#pragma unroll
+        for (int u = 0; u < U; ++u) s_pre[wid][u * 64 + lane] = ptt[u];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const Pos q = pt[i].x - tb;
+          if (q < T) {
+            const uint32_t k = (uint32_t)q >> 4;
+            pt[i].t = s_pre[wid][k] + seg_part<true>(s_data[wid][k], (uint32_t)q & 15u);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+      if (!(RX && i == 1) && pt[i].x - tb == T) pt[i].p = carry_l;
+    if (exact) {
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+        if (pt[i].x - tb == T) pt[i].t = carry_t;
+    }
+
+    if (!last) {
+      ++t;
+      return false;
+    }
+    // end sums: the next lane's start (ragged), else this lane's end point
+    const int nl = (int)(lane < 63u ? lane + 1u : 63u);
+    const uint32_t nx_p = (uint32_t)__shfl((int)pt[0].p, nl, 64);
+    const uint32_t nx_t = (uint32_t)__shfl((int)pt[0].t, nl, 64);
+    const bool own_end = !contig || (!kMarker && lane == 63u);
+    const uint32_t p3 = RX && rx.tnext ? nx_p : pt[3].p;  // P(transport end)
+    const uint32_t pe = own_end ? pt[1].p : nx_p;
+    const uint32_t te = own_end ? pt[1].t : nx_t;
+    const uint64_t p = ch * CH + lane;
+    // TX in place (wbk): this lane's field offset in the tile (wf: it has one),
+    // its line when stored whole (64: not), its value
+    Pos wq = 0;
+    bool wf = false;
+    uint32_t wl = 64u, wr = 0u;
+    Pos x0 = 0;  // the chunk's start (wbk: the TX kind, 32-bit)
+    if (wbk) x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);
+    if (lane < (uint32_t)CH && p < A.n) {
+      const uint32_t odd = (uint32_t)pt[0].x & 1u;
+      if (DG) {
+        // IPv4 header field: ^Checksum(b[:HeaderLength()]) with the field as 0
+        // (network/ipv4/ipv4.go:85-94); transport field: the sender's value
+        // over b[HeaderLength():TotalLength()] with its field as 0 and the
+        // pseudo header + length from the datagram (sendUDP / sendTCP /
+        // sendICMPv4, see include/yucsum.h)
+        uint32_t ip = 0u, l4 = 0u;
+        const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
+        if (rx.hl) ip = ~fold32(le_to_be(p2 - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
+        if (rx.fo) l4 = ~fold32(le_to_be(p3 - p2 - fsum, odd) + rx.pseudo) & 0xFFFFu;
+        if (A.out) {  // out[2p], out[2p + 1]: one 32-bit store when aligned
+          if (((uintptr_t)A.out & 3u) == 0u) {
+            ((uint32_t *)A.out)[p] = ip | (l4 << 16);
+          } else {
+            A.out[2u * p] = (uint16_t)ip;
+            A.out[2u * p + 1u] = (uint16_t)l4;
+          }
+        }
+        if (A.fill) {
+          uint8_t *pk = A.fill + (cur.b0 + pt[0].x - data);
+          if (rx.hl) put_be16(pk + 10u, ip);
+          if (rx.fo) put_be16(pk + rx.fo, l4);
+        }
+      } else if (RX) {
+        // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
+        // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
+        uint32_t r = rx.flags;
         if (!(r & YU_RX_INVALID)) {
-          // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
-          // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
-          const uint32_t odd = x & 1u;
-          const uint32_t p2 = rx.h20 ? p0 + rx.hsum : seg_point<false>(pre2, half, x + hl);
-          const uint32_t ip = fold32(le_to_be(p2 - p0, odd));
+          const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
+          const uint32_t ip = fold32(le_to_be(p2 - pt[0].p, odd));
           if (ip == 0u || ip == 0xFFFFu) r |= YU_RX_IP_OK;
           if (r & YU_RX_L4) {
-            const uint32_t p3 = tl == len && lane < 63u ? pn : seg_point<false>(pre2, half, x + tl);
             const uint32_t l4 = fold32(le_to_be(p3 - p2, odd) + rx.pseudo);
             if (l4 == 0u || l4 == 0xFFFFu) r |= YU_RX_L4_OK;
           }
         }
+        if (A.out) A.out[p] = (uint16_t)r;
+      } else {
+        uint32_t v;
+        if (exact) {
+          const uint32_t L = pe - pt[0].p;
+          const uint32_t S = te - pt[0].t;
+          const uint32_t b = (L - S) * kInv255;  // odd-address bytes
+          const uint32_t a = S - b;              // even-address bytes
+          v = odd ? a + (b << 8) : (a << 8) + b;
+        } else {
+          v = le_to_be(pe - pt[0].p - (tx ? fsum : 0u), odd);
+        }
+        const uint64_t len = plen;
+        uint8_t *pk = A.fill ? A.fill + (cur.b0 + pt[0].x - data) : nullptr;
+        if (tx && wbk && park && fld + 2u <= len) {
+          // the field's offset in the parked (last) tile, wrapping below it;
+          // its line is stored whole below when the field lies in one line of
+          // this tile that holds no byte outside this chunk
+          wq = pt[0].x + fld - tb;
+          wf = true;
+          const Pos ls = wq & ~(Pos)127;
+          // (wq wraps for a field in an earlier tile: wq <= T - 2 keeps those out,
+          // a field ending right at this tile's start included)
+          if (wq <= T - 2u && (wq & 127u) != 127u && tb + ls >= x0 && tb + ls + 128u <= cur.xe) {
+            wl = (uint32_t)wq >> 7;
+            pk = nullptr;  // no 2-byte store
+          }
+        }
+        const uint32_t r = packet_value(A, v, len, cur.sd);
+        if (A.out) A.out[p] = (uint16_t)r;
+        wr = r;
+        if (pk) store_field(A, r, pk, (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
       }
-      const uint64_t p = ch * CH + lane;
-      if (lane < (uint32_t)CH && p < A.n && A.out) A.out[p] = (uint16_t)r;
-    } else {
-
-      const Pos tb = (Pos)(t * T);
-      bool here = false;  // a packet boundary (or header) lies in this tile
-#pragma unroll
-      for (int i = 0; i < NP; ++i)
-        if (!(RX && i == 1)) here |= pt[i].x - tb < T;  // (RX and DG have no end point)
-      if (FB) here |= fx - tb < T;
-      if (RX) {  // a header window [floor4(start), +24) still being gathered
-        const Pos hs = pt[0].x & ~(Pos)3;
-        here |= rx.need != 0u && hs < tb + T && hs + 24u > tb;
-      }
-      const bool park = __any((int)here);
-      // chunk sums, address-ordered exclusive prefixes (DPP scan per u). The TX
-      // kind parks each column as its scan completes (FUSE: no prefix array
-      // live across the scan, registers its in-place write-back needs); the
-      // others after the scan
-      constexpr bool FUSE = K == kSegTx;
-      // chunk prefix; HP: also the chunk's first half's sum (half-chunk prefixes)
-      uint32_t pl[U], ph[U], ptt[U];
+    }
+    if (tx && wbk && park) {  // wave-uniform: the in-place write-back
+      // 1. Every field byte that lies in the tile goes into its parked copy, the
+      //    ones left to their 2-byte stores too (same bytes: a line stored whole
+      //    that holds one stays right).
+      uint8_t *sb = (uint8_t *)s_data[wid];
+      if (wf && wq < T) sb[wq] = (uint8_t)(wr >> 8);
+      if (wf && wq + 1u < T) sb[wq + 1u] = (uint8_t)wr;  // (wq + 1 == 0: a field from the tile before)
+      // 2. The lines holding a field of their own, as a 64-bit mask (T / 128 <= 64 lines).
+      const uint64_t m = (uint64_t)wave_or(wl < 32u ? 1u << wl : 0u) |
+                         ((uint64_t)wave_or(wl >= 32u && wl < 64u ? 1u << (wl - 32u) : 0u) << 32);
+      wave_lds_fence();
+      // 3. Those lines from the tile copy, as full-line 16-byte stores (8 lanes
+      //    per line, one contiguous KiB per instruction), non-temporal. Memory
+      //    then sees whole lines, not one partial write per field.
+      const __amdgpu_buffer_rsrc_t wr_r = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(A.fill + (cur.b0 + tb - data)), (short)0, (int)T, 0x00020000);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        ph[u] = sad(c[u].y, sad(c[u].x, 0u));
-        const uint32_t s = sad(c[u].w, sad(c[u].z, ph[u]));
-        const uint32_t inc = group_total<64>(s);
-        pl[u] = carry_l + inc - s;
-        carry_l += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        if (FUSE && park) {
-          s_data[wid][u * 64 + lane] = c[u];
-          ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl[u], pl[u] + ph[u]);
-        }
-      }
-      if (exact) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          uint32_t s = __builtin_amdgcn_sad_u8(c[u].x, 0u, 0u);
-          s = __builtin_amdgcn_sad_u8(c[u].y, 0u, s);
-          s = __builtin_amdgcn_sad_u8(c[u].z, 0u, s);
-          s = __builtin_amdgcn_sad_u8(c[u].w, 0u, s);
-          const uint32_t inc = group_total<64>(s);
-          ptt[u] = carry_t + inc - s;
-          carry_t += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        }
-      }
-      if (park) {
-        if (!FUSE) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            s_data[wid][u * 64 + lane] = c[u];
-            if (HP)
-              ((uint2 *)s_pre[wid])[u * 64 + lane] = make_uint2(pl[u], pl[u] + ph[u]);
-            else
-              s_pre[wid][u * 64 + lane] = pl[u];
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        bool parsed = false;
-        if (RX && rx.need) {  // gather header dwords held by this tile, parse
-          const Pos q0 = (pt[0].x & ~(Pos)3) - tb;
-          if (q0 <= (Pos)(T - 24u)) {
-            // the whole 24-byte window lies in this tile (q0 wraps past T when
-            // the window began in an earlier one): six reads, no bookkeeping
-            const uint32_t d = (uint32_t)q0 >> 2;
-#pragma unroll
-            for (int j = 0; j < 6; ++j) rx.h[j] = s_dw[d + (uint32_t)j];
-            rx.need = 0u;
-          } else {  // a window across two tiles: the dwords this one holds
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-              const Pos q = q0 + 4u * (uint32_t)j;
-              if (((rx.need >> j) & 1u) && q < T) {
-                rx.h[j] = s_dw[(uint32_t)q >> 2];
-                rx.need &= ~(1u << j);
-              }
-            }
-          }
-          if (rx.need == 0u) {
-            uint32_t hl, tl;
-            rx_parse(rx, (uint32_t)pt[0].x & 3u, plen, hl, tl);
-            // a well-formed datagram fills its packet: in a ragged chunk its
-            // transport end is the next lane's start (the marker lane's, for the
-            // chunk's last packet), already evaluated; when every lane's is, the
-            // wave skips the transport-end slot altogether
-            rx.tnext = contig && kMarker && tl == (uint32_t)plen ? 1u : 0u;
-            if (DG) {
-              // in contract HeaderLength() >= 20: every point lies at or past
-              // byte 20, so never in a tile that has gone by
-              const uint32_t fo = dg_parse(rx, (uint32_t)pt[0].x & 3u, hl, tl);
-              if (rx.hl) {
-                pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
-                pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
-              }
-              if (fo) {
-                fx = pt[0].x + fo;
-                fk = 2u;
-              }
-            } else {
-              pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
-              pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
-            }
-            parsed = true;
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < NP; ++i) {
-          const Pos q = pt[i].x - tb;
-          if (!(RX && i == 1) && q < T) {
-            if (HP) {
-              pt[i].p = seg_point<false>(s_pre[wid], (const uint2 *)s_data[wid], (uint32_t)q);
-            } else {
-              const uint32_t k = (uint32_t)q >> 4;
-              pt[i].p = s_pre[wid][k] + seg_part<false>(s_data[wid][k], (uint32_t)q & 15u);
-            }
-          }
-        }
-        if (FB) {  // the field's bytes, weighted by address parity
-          const Pos q = fx - tb;
-          if (q < T) {
-            const uint8_t *sb = (const uint8_t *)s_data[wid];
-            const uint32_t b = sb[q];
-            fsum += (q & 1u) ? b << 8 : b;
-            if (fk == 2u && q + 1u < T) {
-              const uint32_t b1 = sb[q + 1u];
-              fsum += (q & 1u) ? b1 : b1 << 8;
-            }
-            const bool split = fk == 2u && q + 1u == T;  // the field's second byte opens the next tile
-            fk = split ? 1u : 0u;
-            fx = split ? fx + 1u : kNoPt;
-          }
-        }
-        if (RX && !DG && parsed) {
-          // A header straddling two tiles is parsed in the second, but a header
-          // or total length under 20 bytes (IsValid accepts IHL 0..4) can put
-          // its point in the first, whose bytes have gone by. Such a point lies
-          // inside the gathered 24-byte window: P(point) = P(start) + the LE sum
-          // of the window bytes in between, taken from the registers.
-          const uint32_t sh = (uint32_t)pt[0].x & 3u;
-#pragma unroll
-          for (int i = 2; i < 4; ++i) {
-            if (pt[i].x < tb) {
-              const uint32_t b = sh + (uint32_t)(pt[i].x - pt[0].x);  // < sh + 20
-              uint32_t s = pt[0].p;
-#pragma unroll
-              for (int j = 0; j < 6; ++j)
-                s = sad(rx.h[j] & byte_range_mask(4u * (uint32_t)j, sh, b), s);
-              pt[i].p = s;
-            }
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (exact) {  // second pass, same buffer: the byte-sum prefixes
-#pragma unroll
-          for (int u = 0; u < U; ++u) s_pre[wid][u * 64 + lane] = ptt[u];
-          __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int i = 0; i < NP; ++i) {
-            const Pos q = pt[i].x - tb;
-            if (q < T) {
-              const uint32_t k = (uint32_t)q >> 4;
-              pt[i].t = s_pre[wid][k] + seg_part<true>(s_data[wid][k], (uint32_t)q & 15u);
-            }
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NP; ++i)
-        if (!(RX && i == 1) && pt[i].x - tb == T) pt[i].p = carry_l;
-      if (exact) {
-#pragma unroll
-        for (int i = 0; i < NP; ++i)
-          if (pt[i].x - tb == T) pt[i].t = carry_t;
-      }
-
-      if (!last) {
-        ++t;
-        return false;
-      }
-      // end sums: the next lane's start (ragged), else this lane's end point
-      const int nl = (int)(lane < 63u ? lane + 1u : 63u);
-      const uint32_t nx_p = (uint32_t)__shfl((int)pt[0].p, nl, 64);
-      const uint32_t nx_t = (uint32_t)__shfl((int)pt[0].t, nl, 64);
-      const bool own_end = !contig || (!kMarker && lane == 63u);
-      const uint32_t p3 = RX && rx.tnext ? nx_p : pt[3].p;  // P(transport end)
-      const uint32_t pe = own_end ? pt[1].p : nx_p;
-      const uint32_t te = own_end ? pt[1].t : nx_t;
-      const uint64_t p = ch * CH + lane;
-      // TX in place (wbk): this lane's field offset in the tile (wf: it has one),
-      // its line when stored whole (64: not), its value
-      Pos wq = 0;
-      bool wf = false;
-      uint32_t wl = 64u, wr = 0u;
-      Pos x0 = 0;  // the chunk's start (wbk: the TX kind, 32-bit)
-      if (wbk) x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);
-      if (lane < (uint32_t)CH && p < A.n) {
-        const uint32_t odd = (uint32_t)pt[0].x & 1u;
-        if (DG) {
-          // IPv4 header field: ^Checksum(b[:HeaderLength()]) with the field as 0
-          // (network/ipv4/ipv4.go:85-94); transport field: the sender's value
-          // over b[HeaderLength():TotalLength()] with its field as 0 and the
-          // pseudo header + length from the datagram (sendUDP / sendTCP /
-          // sendICMPv4, see include/yucsum.h)
-          uint32_t ip = 0u, l4 = 0u;
-          const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
-          if (rx.hl) ip = ~fold32(le_to_be(p2 - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
-          if (rx.fo) l4 = ~fold32(le_to_be(p3 - p2 - fsum, odd) + rx.pseudo) & 0xFFFFu;
-          if (A.out) {  // out[2p], out[2p + 1]: one 32-bit store when aligned
-            if (((uintptr_t)A.out & 3u) == 0u) {
-              ((uint32_t *)A.out)[p] = ip | (l4 << 16);
-            } else {
-              A.out[2u * p] = (uint16_t)ip;
-              A.out[2u * p + 1u] = (uint16_t)l4;
-            }
-          }
-          if (A.fill) {
-            uint8_t *pk = A.fill + (cur.b0 + pt[0].x - data);
-            if (rx.hl) put_be16(pk + 10u, ip);
-            if (rx.fo) put_be16(pk + rx.fo, l4);
-          }
-        } else if (RX) {
-          // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
-          // pseudo + BE16(len) + segment in {0, 0xffff} (checker/checker.go:32-35,80-92)
-          uint32_t r = rx.flags;
-          if (!(r & YU_RX_INVALID)) {
-            const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
-            const uint32_t ip = fold32(le_to_be(p2 - pt[0].p, odd));
-            if (ip == 0u || ip == 0xFFFFu) r |= YU_RX_IP_OK;
-            if (r & YU_RX_L4) {
-              const uint32_t l4 = fold32(le_to_be(p3 - p2, odd) + rx.pseudo);
-              if (l4 == 0u || l4 == 0xFFFFu) r |= YU_RX_L4_OK;
-            }
-          }
-          if (A.out) A.out[p] = (uint16_t)r;
-        } else {
-          uint32_t v;
-          if (exact) {
-            const uint32_t L = pe - pt[0].p;
-            const uint32_t S = te - pt[0].t;
-            const uint32_t b = (L - S) * kInv255;  // odd-address bytes
-            const uint32_t a = S - b;              // even-address bytes
-            v = odd ? a + (b << 8) : (a << 8) + b;
-          } else {
-            v = le_to_be(pe - pt[0].p - (tx ? fsum : 0u), odd);
-          }
-          const uint64_t len = plen;
-          uint8_t *pk = A.fill ? A.fill + (cur.b0 + pt[0].x - data) : nullptr;
-          if (tx && wbk && park && fld + 2u <= len) {
-            // the field's offset in the parked (last) tile, wrapping below it;
-            // its line is stored whole below when the field lies in one line of
-            // this tile that holds no byte outside this chunk
-            wq = pt[0].x + fld - tb;
-            wf = true;
-            const Pos ls = wq & ~(Pos)127;
-            // (wq wraps for a field in an earlier tile: wq <= T - 2 keeps those out,
-            // a field ending right at this tile's start included)
-            if (wq <= T - 2u && (wq & 127u) != 127u && tb + ls >= x0 && tb + ls + 128u <= cur.xe) {
-              wl = (uint32_t)wq >> 7;
-              pk = nullptr;  // no 2-byte store
-            }
-          }
-          const uint32_t r = packet_value(A, v, len, cur.sd);
-          if (A.out) A.out[p] = (uint16_t)r;
-          wr = r;
-          if (pk) store_field(A, r, pk, (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
-        }
-      }
-      if (tx && wbk && park) {  // wave-uniform: the in-place write-back
-        // 1. Every field byte that lies in the tile goes into its parked copy, the
-        //    ones left to their 2-byte stores too (same bytes: a line stored whole
-        //    that holds one stays right).
-        uint8_t *sb = (uint8_t *)s_data[wid];
-        if (wf && wq < T) sb[wq] = (uint8_t)(wr >> 8);
-        if (wf && wq + 1u < T) sb[wq + 1u] = (uint8_t)wr;  // (wq + 1 == 0: a field from the tile before)
-        // 2. The lines holding a field of their own, as a 64-bit mask (T / 128 <= 64 lines).
-        const uint64_t m = (uint64_t)wave_or(wl < 32u ? 1u << wl : 0u) |
-                           ((uint64_t)wave_or(wl >= 32u && wl < 64u ? 1u << (wl - 32u) : 0u) << 32);
-        wave_lds_fence();
-        // 3. Those lines from the tile copy, as full-line 16-byte stores (8 lanes
-        //    per line, one contiguous KiB per instruction), non-temporal. Memory
-        //    then sees whole lines, not one partial write per field.
-        const __amdgpu_buffer_rsrc_t wr_r = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(A.fill + (cur.b0 + tb - data)), (short)0, (int)T, 0x00020000);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const uint32_t k = (uint32_t)u * 64u + lane;
-          const uint4 d = s_data[wid][k];
-          const uint32_t off = ((m >> (k >> 3)) & 1u) ? 16u * k : kOOB;
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 2);  // nt
-        }
+        const uint32_t k = (uint32_t)u * 64u + lane;
+        const uint4 d = s_data[wid][k];
+        const uint32_t off = ((m >> (k >> 3)) & 1u) ? 16u * k : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 2);  // nt
       }
     }
     if ((ch + nwave) * CH >= A.n) return true;
@@ -2353,6 +2306,10 @@ const Variant kSegRx8 = YU_SEG(8, kSegRx, "k_seg<8,rx>");
 // 16-packet chunks: 4x the waves for mid-size ragged batches (see pick_ragged)
 const Variant kSeg8c16 = YU_SEG16(8, kSegPlain, "k_seg<8,c16>");
 const Variant kSegTx8c16 = YU_SEG16(8, kSegTx, "k_seg<8,tx,c16>");
+// the TX kinds' in-place form for ragged batches (the whole-line write-back)
+const Variant kSegTxW4 = YU_SEG(4, kSegTxW, "k_seg<4,txw>");
+const Variant kSegTxW8 = YU_SEG(8, kSegTxW, "k_seg<8,txw>");
+const Variant kSegTxW8c16 = YU_SEG16(8, kSegTxW, "k_seg<8,txw,c16>");
 const Variant kSegRx8c16 = YU_SEG16(8, kSegRx, "k_seg<8,rx,c16>");
 // (no 4 KiB-tile DG kind: datagram batches take the ragged picks, 8 KiB)
 const Variant kSegDg8 = YU_SEG(8, kSegDg, "k_seg<8,dg>");
@@ -2617,6 +2574,17 @@ int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
   return YU_OK;
 }
 
+// Ragged in place: the TX kinds of k_seg take their TXW form (the whole-line
+// write-back, 1M UDP datagrams U{40..200}: 62.3 -> 48.1 us) unless YU_FILL_WB=0.
+const Variant &pick_ragged_fill(int mode, uint64_t n, bool fill) {
+  const Variant &v = pick_ragged(mode, n);
+  if (!fill || !fill_wb()) return v;
+  if (&v == &kSegTx8) return kSegTxW8;
+  if (&v == &kSegTx8c16) return kSegTxW8c16;
+  if (&v == &kSegTx4) return kSegTxW4;
+  return v;
+}
+
 int batch_uniform(const uint8_t *data, uint8_t *fill, uint64_t stride,
                   uint32_t len, uint64_t n, int mode,
                   const uint16_t *initial_arr, uint16_t initial,
@@ -2674,11 +2642,11 @@ int batch_ragged(const uint8_t *data, uint8_t *fill, const uint64_t *offsets,
   A.end = 0;
   A.len = 0;
   A.initial = initial;
-  A.uf = fill && mode_is_tx(mode) ? (uint32_t)fill_wb() : 0u;  // k_seg TX kind: the write-back
+  A.uf = 0;
   A.mode = mode;
   // k_seg streams the batch's bytes (exact BE recovery for chunks holding a
   // RAW packet > 131072 bytes); k_rag takes the IPv4 header-only modes.
-  return launch(pick_ragged(mode, n), A, (hipStream_t)stream);
+  return launch(pick_ragged_fill(mode, n, fill != nullptr), A, (hipStream_t)stream);
 }
 
 // Completion signal for the host path's direct mode (yucsum_internal.h):
@@ -2753,6 +2721,11 @@ const char *yu_ragged_variant(int mode) {
 const char *yu_ragged_variant_n(int mode, uint64_t n) {
   if (mode < 0 || mode >= YU_MODE_COUNT) return "";
   return pick_ragged(mode, n).name;
+}
+
+const char *yu_ragged_fill_variant_n(int mode, uint64_t n) {
+  if (mode < 0 || mode >= YU_MODE_COUNT) return "";
+  return pick_ragged_fill(mode, n, true).name;
 }
 
 int yu_device_count(void) {
