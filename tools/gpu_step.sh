@@ -1,7 +1,7 @@
-# round 4, call E: k_seg with the in-place TXW kind (whole-line write-back) and the
-# on 32-bit chunk loads with the park fused into its scan (and the whole-line
-# the write-back off, kbench A/B
-# against the round-start library (tools/old), the driver-style bench line
+# round 4, call E: k_seg with the in-place TXW kind (whole-line write-back), the other
+# kinds as at round start (the RX one-tile path reverted): GPU suite, the fill tests
+# with the write-back off, kbench A/B against the round-start library (tools/old),
+# the driver-style bench line, trace + PMC passes of configs 12 and 13
 set -o pipefail
 mkdir -p gpurun_out
 T=r04e
