@@ -5,10 +5,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 T=r04e
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1 || { tail -60 gpurun_out/gpu_tests_$T.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_$T.log
-YU_FILL_WB=0 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "fill or fuzz or kernel_verified" --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_${T}_wb0.log 2>&1 || { tail -40 gpurun_out/gpu_tests_${T}_wb0.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_${T}_wb0.log
+#timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1 || { tail -60 gpurun_out/gpu_tests_$T.log; exit 1; }
+#tail -1 gpurun_out/gpu_tests_$T.log
+#YU_FILL_WB=0 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "fill or fuzz or kernel_verified" --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_${T}_wb0.log 2>&1 || { tail -40 gpurun_out/gpu_tests_${T}_wb0.log; exit 1; }
+#tail -1 gpurun_out/gpu_tests_${T}_wb0.log
 O=LD_LIBRARY_PATH=tools/old
 F="KB_FILL=1 KB_ALIGN4=1"
 timeout -k 10 900 bash tools/ab.sh "16 $O" "16" "16 $O" "16" "16 $O" "16" "8 $O" "8" "8 $O" "8" "6 $O" "6" "5 $O" "5" "4 $O" "4" \

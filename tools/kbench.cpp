@@ -17,6 +17,9 @@
 
 #include "yucsum.h"
 
+// weak: an A/B against an older library (LD_LIBRARY_PATH=tools/old) may lack it
+#pragma weak yu_ragged_fill_variant_n
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1);} } while (0)
 
@@ -172,7 +175,7 @@ int main(int argc, char **argv) {
       double s = ms / 1e3 / reps;
       printf("config%d round %d: %8.1f us/launch  %7.1f GB/s alg  (%.3f of 8 TB/s)  %s\n", cfg, r, s * 1e6,
              alg / s / 1e9, alg / s / 8e12,
-             d_off ? (fill ? yu_ragged_fill_variant_n(mode, n) : yu_ragged_variant_n(mode, n))
+             d_off ? (fill && yu_ragged_fill_variant_n ? yu_ragged_fill_variant_n(mode, n) : yu_ragged_variant_n(mode, n))
                    : yu_uniform_variant_n(L, L, n, mode, (uintptr_t)bufs[0] & 15));
     }
     for (auto b : bufs) CK(hipFree(b));
