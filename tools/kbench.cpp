@@ -2,7 +2,7 @@
 // points on BASELINE configs 2/3/4 with HIP events, without Python/torch in
 // the loop, for quick kernel A/B work and rocprofv3 runs.
 //
-// build: hipcc -O2 --offload-arch=gfx950 -I include tools/kbench.cpp -o tools/kbench -L yustack_amd -lyucsum -Wl,-rpath,'$ORIGIN/../yustack_amd'
+// build: hipcc -O2 --offload-arch=gfx950 -I include tools/kbench.cpp -o tools/kbench -L yustack_amd -lyucsum -ldl -Wl,-rpath,'$ORIGIN/../yustack_amd'
 // run:   tools/kbench [config...]   (default 2 3 4; 14 reads KB_LEN)
 #include <hip/hip_runtime.h>
 #include <execinfo.h>
@@ -16,9 +16,7 @@
 #include <vector>
 
 #include "yucsum.h"
-
-// weak: an A/B against an older library (LD_LIBRARY_PATH=tools/old) may lack it
-#pragma weak yu_ragged_fill_variant_n
+#include <dlfcn.h>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1);} } while (0)
@@ -77,6 +75,9 @@ int main(int argc, char **argv) {
   // KB_N: packets per batch (default 1M)
   const uint64_t n = getenv("KB_N") ? strtoull(getenv("KB_N"), nullptr, 10) : 1ull << 20;
   const int reps = 30, rounds = 3;
+  // looked up at run time: an A/B against an older library (LD_LIBRARY_PATH=tools/old) lacks it
+  typedef const char *(*name_fn)(int, uint64_t);
+  const name_fn fill_name = (name_fn)dlsym(RTLD_DEFAULT, "yu_ragged_fill_variant_n");
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -175,7 +176,7 @@ int main(int argc, char **argv) {
       double s = ms / 1e3 / reps;
       printf("config%d round %d: %8.1f us/launch  %7.1f GB/s alg  (%.3f of 8 TB/s)  %s\n", cfg, r, s * 1e6,
              alg / s / 1e9, alg / s / 8e12,
-             d_off ? (fill && yu_ragged_fill_variant_n ? yu_ragged_fill_variant_n(mode, n) : yu_ragged_variant_n(mode, n))
+             d_off ? (fill && fill_name ? fill_name(mode, n) : yu_ragged_variant_n(mode, n))
                    : yu_uniform_variant_n(L, L, n, mode, (uintptr_t)bufs[0] & 15));
     }
     for (auto b : bufs) CK(hipFree(b));
