@@ -59,7 +59,7 @@ def main(prof_dir, out_path):
     if os.path.exists(out_path):  # merge: configs not profiled in prof_dir keep their record
         with open(out_path) as f:
             res = json.load(f)
-    for c in ("2", "3", "4", "6", "7", "8", "9", "10", "11"):
+    for c in ("2", "3", "4", "6", "7", "8", "9", "10", "11", "12", "13"):
         cfg = f"config{c}"
         fpath = os.path.join(prof_dir, f"pmc_FETCH_SIZE_c{c}", "run_counter_collection.csv")
         wpath = os.path.join(prof_dir, f"pmc_WRITE_SIZE_c{c}", "run_counter_collection.csv")
