@@ -1,20 +1,14 @@
-# round 4, call E: k_seg with the in-place TXW kind (whole-line write-back), the other
-# kinds as at round start (the RX one-tile path reverted): GPU suite, the fill tests
-# with the write-back off, kbench A/B against the round-start library (tools/old),
-# the driver-style bench line, trace + PMC passes of configs 12 and 13
+# round 4, call F: SQ instruction / stall counters of config 7's kernel (kbench 16):
+# the round-start RX kind (tools/old) against the one-tile straight-line path
+# (tools/rxfast, side build of 3e46d4c) -- did that path cut instructions?
 set -o pipefail
 mkdir -p gpurun_out
-T=r04e
-#timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1 || { tail -60 gpurun_out/gpu_tests_$T.log; exit 1; }
-#tail -1 gpurun_out/gpu_tests_$T.log
-#YU_FILL_WB=0 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "fill or fuzz or kernel_verified" --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_${T}_wb0.log 2>&1 || { tail -40 gpurun_out/gpu_tests_${T}_wb0.log; exit 1; }
-#tail -1 gpurun_out/gpu_tests_${T}_wb0.log
-O=LD_LIBRARY_PATH=tools/old
-F="KB_FILL=1 KB_ALIGN4=1"
-timeout -k 10 900 bash tools/ab.sh "16 $O" "16" "16 $O" "16" "16 $O" "16" "8 $O" "8" "8 $O" "8" "6 $O" "6" "5 $O" "5" "4 $O" "4" \
-  "15 $O" "15" "15 KB_MODE=8 $O" "15 KB_MODE=8" "8 $F $O" "8 $F" "8 $F $O" "8 $F" "7 $F $O" "7 $F" > gpurun_out/kbench_ab_$T.log 2>&1 || { tail gpurun_out/kbench_ab_$T.log; exit 1; }
-grep -E "^==|round 2" gpurun_out/kbench_ab_$T.log
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || { tail gpurun_out/bench_$T.err; exit 1; }
-python -c "import json;d=json.load(open('gpurun_out/bench_$T.json'));print(d['value'],d['roofline']['frac']);[print(k,v['kernel_avg_us'],v['roofline_frac']) for k,v in d['other_configs'].items()]"
-CFGS="12 13" timeout -k 10 600 bash tools/profile.sh $T || exit 1
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+C1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"
+C2="SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_INSTS_BRANCH"
+for lib in old rxfast; do
+  TAG=_${lib}_a SQ_COUNTERS="$C1" bash tools/pmc_sq.sh 16 LD_LIBRARY_PATH=$R/tools/$lib || exit 1
+  TAG=_${lib}_b SQ_COUNTERS="$C2" bash tools/pmc_sq.sh 16 LD_LIBRARY_PATH=$R/tools/$lib || exit 1
+done
+python3 tools/sq_summary.py gpurun_out/sq_16_old_a gpurun_out/sq_16_rxfast_a gpurun_out/sq_16_old_b gpurun_out/sq_16_rxfast_b
 echo ok
