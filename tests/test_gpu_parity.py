@@ -1299,7 +1299,7 @@ def test_random_batches_fuzz(dev, oracle_c):
             _fuzz_headers(rng, blob, offs[:-1], lens, mode)
             want = oracle_c.batch(blob, mode, offsets=offs, initial_arr=init, initial=initial, addrs=addrs)
             d = _to(dev, blob)
-            seen.add(batch.ragged_variant(mode, n))
+            seen.add(batch.ragged_variant(mode, n, fill=fill))
             got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), mode, initial=initial,
                                         initial_arr=None if init is None else _to(dev, init),
                                         addrs=None if addrs is None else _to(dev, addrs),
