@@ -35,7 +35,7 @@ def tokens():
         p = os.path.join(ROOT, d)
         if not os.path.exists(p):
             continue
-        for t in re.findall(r"`([^`\n]+)`", open(p).read()):
+        for t in re.findall(r"`([^`]+)`", open(p).read()):
             for part in t.split():
                 part = part.strip(",;:()")
                 if part.startswith("profiles/"):
