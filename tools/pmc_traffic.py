@@ -32,7 +32,7 @@ def short_name(full):
     if k == "k_loop":
         return f"k_loop<{args[0]},{'BE' if args[2] == 'true' else 'LE'}>"
     if k == "k_seg":
-        kind = {"2": ",rx", "true": ",rx", "1": ",tx", "3": ",dg", "4": ",txw", "5": ",dgw"}.get(args[2], "")  # template K
+        kind = {"2": ",rx", "true": ",rx", "1": ",tx", "3": ",dg", "4": ",txw"}.get(args[2], "")  # template K
         return f"k_seg<{args[0]}{kind}>"
     if k == "k_rag":
         return f"k_rag<{args[0]},{args[1]}>"

@@ -379,7 +379,7 @@ __device__ __forceinline__ uint32_t packet_value(const BatchArgs &A, uint32_t v,
 __device__ __forceinline__ void store_field(const BatchArgs &A, uint32_t r, uint8_t *pkt,
                                             uint32_t hdr_end) {
   const int mode = A.mode;
-  if (A.fill && pkt && mode_is_tx(mode)) {
+  if (A.fill && mode_is_tx(mode)) {
     const uint32_t f = mode_field(mode);
     if (f + 2u <= hdr_end) {
       // binary.BigEndian.PutUint16: one 16-bit store when the field is
@@ -1680,19 +1680,15 @@ constexpr int kSegPlain = 0, kSegTx = 1, kSegRx = 2, kSegDg = 3;
 // write-back needs; TX itself keeps the layout that serves its result-array
 // form best, 26.1 vs 26.8 us on kbench 8)
 constexpr int kSegTxW = 4;
-// DGW: TX_DATAGRAM the same way (both fields of whole datagrams in place)
-constexpr int kSegDgW = 5;
 
 // (the DG kind asks for at least 3 waves per SIMD, which it would otherwise
 // miss by a few VGPRs; the other kinds are left alone)
 template <int U, int NT, int K, int CH = 64>
-__global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_seg(BatchArgs A) {
-  constexpr bool DGW = K == kSegDgW;
-  constexpr bool DG = K == kSegDg || DGW;
+__global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
+  constexpr bool DG = K == kSegDg;
   constexpr bool RX = K == kSegRx || DG;  // parses each packet's IPv4 header
   constexpr bool TXW = K == kSegTxW;
   constexpr bool tx = K == kSegTx || TXW;
-  constexpr bool WB = TXW || DGW;  // the in-place kinds with the whole-line write-back
   constexpr bool FB = tx || DG;                 // a field whose bytes are read from the tile
   constexpr int NP = K == kSegRx || DG ? 4 : 2;  // point slots in use
   constexpr uint32_t T = 64u * 16u * U;
@@ -1712,10 +1708,10 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
   const uint64_t end = A.offsets ? data + A.offsets[A.n] : A.end;
   const uint32_t *s_dw = (const uint32_t *)s_data[wid];
   const bool contig = A.offsets != nullptr;  // ragged: packets back to back
-  // TXW / DGW kinds (writing a ragged batch in place): fields whose values are
-  // final go into the parked tile they lie in, and its 128-byte lines that hold
-  // them are stored back whole with non-temporal stores (wb_tile).
-  const bool wbk = WB && A.fill && contig;
+  // TXW kind (writing a ragged batch in place): the fields go into the parked
+  // last tile of each chunk and its whole 128-byte lines are stored back with
+  // non-temporal stores. See the chunk epilogue.
+  const bool wbk = TXW && A.fill && contig;
   // Positions relative to the chunk's b0: 64-bit for the plain kind (RAW packets
   // up to YU_MAX_RAW_LEN), 32-bit for the TX / RX / DG kinds, whose packets are
   // at most 65535 bytes (include/yucsum.h), so a 64-packet chunk spans < 4.2 MB
@@ -1732,7 +1728,7 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
 
   uint64_t ch = wave;
   if (wave >= nwave || ch * CH >= A.n) return;
-  using Chunk = typename std::conditional<WB, SegChunk32, SegChunk>::type;
+  using Chunk = typename std::conditional<TXW, SegChunk32, SegChunk>::type;
   Chunk cur, nxt;
   seg_load<CH, !RX>(A, sp, ch * CH, lane, cur);
   seg_load<CH, !RX>(A, sp, (ch + nwave) * CH, lane, nxt);
@@ -1746,6 +1742,11 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
   // zero mask: give it a defined value once, not per chunk.
 #pragma unroll
   for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
+  // A header window that starts 4-aligned and crosses two tiles never gathers
+  // h[5] (its bytes lie past the 20-byte header), yet rx_parse reads it under a
+  // zero mask: give it a defined value once, not per chunk.
+#pragma unroll
+  for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
   // TX, DG: the checksum field's next unread byte (kNoPt: none or done; DG: the
   // transport field), the bytes of it still to read (2, or 1 when the field
   // straddles two tiles) and the address-ordered LE sum of those read:
@@ -1754,22 +1755,14 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
   uint32_t fk = 0, fsum = 0;
   bool exact = false;
   uint32_t carry_l = 0, carry_t = 0;
-  typename std::conditional<WB, uint32_t, uint64_t>::type plen = 0;  // this lane's packet length
-  // in place (wbk): the fields this lane still has to store (bit 0: the TX field
-  // or DG's IPv4 field, bit 1: DG's transport field) and the chunk's first byte
-  uint32_t wpend = 0u;
-  Pos x0 = 0;
+  typename std::conditional<TXW, uint32_t, uint64_t>::type plen = 0;  // this lane's packet length
   auto begin_chunk = [&](const Chunk &k, uint64_t p0) __attribute__((always_inline)) {
-    typename std::conditional<WB, uint32_t, uint64_t>::type x64, len;
+    typename std::conditional<TXW, uint32_t, uint64_t>::type x64, len;
     seg_xlen<CH>(A, k, lane, p0, x64, len);
     plen = len;
     const Pos x = (Pos)x64;
     const Pos y = x + (Pos)len;
     pt[0].x = x;
-    if (WB && wbk) {
-      x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)x, 0, 64);
-      wpend = TXW && fld + 2u <= len ? 1u : 0u;  // DGW: set when the header is parsed
-    }
     // ragged packets lie back to back: P(end) is the next lane's P(start), so
     // only lane 63 evaluates an end point (the chunk end); RX needs none
     pt[1].x = RX || (contig && (kMarker || lane != 63u)) ? kNoPt : y;
@@ -1798,94 +1791,6 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
   };
   begin_chunk(cur, ch * CH);
 
-  // The in-place write-back of the WB kinds, once per parked tile (tile offset
-  // tb), after its points are evaluated: every field whose value is now final
-  // (every sum it needs is known: its packet's end, and for DG the header end)
-  // goes into the tile's LDS copy when it lies there; the 128-byte lines that
-  // hold such a field, lie wholly inside this chunk and hold no field still
-  // waiting for its value are stored back whole; every other final field gets
-  // its 2-byte store now. A line is stored at most once, in its own tile, and
-  // never holds a field that a 2-byte store writes, so no two stores meet.
-  auto wb_tile = [&](Pos tb) __attribute__((always_inline)) {
-    const Pos lim = tb + T;  // points up to the tile's end have their sums
-    const uint32_t odd = (uint32_t)pt[0].x & 1u;
-    const int nl = (int)(lane < 63u ? lane + 1u : 63u);
-    const Pos nx_x = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, nl, 64);
-    const uint32_t nx_p = (uint32_t)__shfl((int)pt[0].p, nl, 64);
-    bool fin;
-    uint32_t v0, v1 = 0u;
-    if (TXW) {  // ragged: the end is the next lane's start (lane 63's own, 64-packet chunks)
-      const bool own_end = !kMarker && lane == 63u;
-      fin = (own_end ? pt[1].x : nx_x) <= lim;
-      const uint32_t pe = own_end ? pt[1].p : nx_p;
-      v0 = packet_value(A, le_to_be(pe - pt[0].p - fsum, odd), plen, cur.sd);
-    } else {  // DGW: the IPv4 field needs the header end, the transport field the datagram end
-      const bool h_ok = rx.h20 || pt[2].x <= lim;
-      fin = h_ok && (!rx.fo || (rx.tnext ? nx_x : pt[3].x) <= lim);
-      const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;
-      const uint32_t p3 = rx.tnext ? nx_p : pt[3].p;
-      v0 = ~fold32(le_to_be(p2 - pt[0].p - rx.ipf, odd)) & 0xFFFFu;
-      v1 = ~fold32(le_to_be(p3 - p2 - fsum, odd) + rx.pseudo) & 0xFFFFu;
-    }
-    fin = fin && wpend != 0u;
-    // field offsets in the tile (wrapping below it)
-    const Pos q0 = pt[0].x + (TXW ? fld : 10u) - tb;
-    const Pos q1 = pt[0].x + rx.fo - tb;
-    uint8_t *sb = (uint8_t *)s_data[wid];
-    auto line_of = [&](Pos q) -> uint32_t {  // its line when the field lies whole in an interior line of the tile
-      const Pos ls = q & ~(Pos)127;
-      return q <= T - 2u && (q & 127u) != 127u && tb + ls >= x0 && tb + ls + 128u <= cur.xe ? (uint32_t)q >> 7
-                                                                                            : 64u;
-    };
-    auto bit = [](Pos q) -> uint64_t { return q < T ? 1ull << ((uint32_t)q >> 7) : 0ull; };
-    uint32_t c0 = 64u, c1 = 64u;  // candidate lines of this lane's final fields
-    uint64_t pend = 0u;           // lines holding a field of this lane still waiting
-    if (wpend & 1u) {
-      if (fin) {
-        if (q0 < T) sb[q0] = (uint8_t)(v0 >> 8);
-        if (q0 + 1u < T) sb[q0 + 1u] = (uint8_t)v0;
-        c0 = line_of(q0);
-      } else {
-        pend |= bit(q0) | bit(q0 + 1u);
-      }
-    }
-    if (DGW && (wpend & 2u)) {
-      if (fin) {
-        if (q1 < T) sb[q1] = (uint8_t)(v1 >> 8);
-        if (q1 + 1u < T) sb[q1 + 1u] = (uint8_t)v1;
-        c1 = line_of(q1);
-      } else {
-        pend |= bit(q1) | bit(q1 + 1u);
-      }
-    }
-    // DGW: a header not yet parsed (it runs into the next tile) may put its
-    // IPv4 field here
-    if (DGW && rx.need) pend |= bit(q0) | bit(q0 + 1u);
-    const uint64_t cand = (c0 < 64u ? 1ull << c0 : 0ull) | (c1 < 64u ? 1ull << c1 : 0ull);
-    const uint64_t dirty = ((uint64_t)wave_or((uint32_t)cand) | ((uint64_t)wave_or((uint32_t)(cand >> 32)) << 32)) &
-                           ~((uint64_t)wave_or((uint32_t)pend) | ((uint64_t)wave_or((uint32_t)(pend >> 32)) << 32));
-    if (fin) {  // final fields no stored line covers: their 2-byte stores
-      uint8_t *pk = A.fill + (cur.b0 + pt[0].x - data);
-      if ((wpend & 1u) && !(c0 < 64u && ((dirty >> c0) & 1u))) put_be16(pk + (TXW ? fld : 10u), v0);
-      if (DGW && (wpend & 2u) && !(c1 < 64u && ((dirty >> c1) & 1u))) put_be16(pk + rx.fo, v1);
-      wpend = 0u;
-    }
-    if (dirty) {  // wave-uniform
-      wave_lds_fence();
-      // full-line 16-byte stores from the tile copy (8 lanes per line, one
-      // contiguous KiB per instruction), non-temporal
-      const __amdgpu_buffer_rsrc_t wr_r = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)(A.fill + (cur.b0 + tb - data)), (short)0, (int)T, 0x00020000);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t k = (uint32_t)u * 64u + lane;
-        const uint4 d = s_data[wid][k];
-        const uint32_t off = ((dirty >> (k >> 3)) & 1u) ? 16u * k : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 2);  // nt
-      }
-    }
-  };
-
   uint64_t t = 0;
   // One tile: issue the loads of the next item into cn, then sum c.
   // Returns true when the wave has no next item.
@@ -1902,6 +1807,7 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
                           end, cn);
 
+
     const Pos tb = (Pos)(t * T);
     bool here = false;  // a packet boundary (or header) lies in this tile
 #pragma unroll
@@ -1917,7 +1823,7 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
     // kind parks each column as its scan completes (FUSE: no prefix array
     // live across the scan, registers its in-place write-back needs); the
     // others after the scan
-    constexpr bool FUSE = WB;
+    constexpr bool FUSE = TXW;
     // chunk prefix; HP: also the chunk's first half's sum (half-chunk prefixes)
     uint32_t pl[U], ph[U], ptt[U];
 #pragma unroll
@@ -1988,7 +1894,6 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
             // in contract HeaderLength() >= 20: every point lies at or past
             // byte 20, so never in a tile that has gone by
             const uint32_t fo = dg_parse(rx, (uint32_t)pt[0].x & 3u, hl, tl);
-            if (DGW && wbk) wpend = (rx.hl ? 1u : 0u) | (fo ? 2u : 0u);
             if (rx.hl) {
               pt[2].x = rx.h20 ? kNoPt : pt[0].x + hl;
               pt[3].x = rx.tnext ? kNoPt : pt[0].x + tl;
@@ -2074,7 +1979,6 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
       for (int i = 0; i < NP; ++i)
         if (pt[i].x - tb == T) pt[i].t = carry_t;
     }
-    if (WB && wbk && park) wb_tile(tb);
 
     if (!last) {
       ++t;
@@ -2089,6 +1993,13 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
     const uint32_t pe = own_end ? pt[1].p : nx_p;
     const uint32_t te = own_end ? pt[1].t : nx_t;
     const uint64_t p = ch * CH + lane;
+    // TX in place (wbk): this lane's field offset in the tile (wf: it has one),
+    // its line when stored whole (64: not), its value
+    Pos wq = 0;
+    bool wf = false;
+    uint32_t wl = 64u, wr = 0u;
+    Pos x0 = 0;  // the chunk's start (wbk: the TX kind, 32-bit)
+    if (wbk) x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);
     if (lane < (uint32_t)CH && p < A.n) {
       const uint32_t odd = (uint32_t)pt[0].x & 1u;
       if (DG) {
@@ -2109,10 +2020,10 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
             A.out[2u * p + 1u] = (uint16_t)l4;
           }
         }
-        if (A.fill) {  // (wbk: the fields wb_tile has not stored, if its last tile did not park)
+        if (A.fill) {
           uint8_t *pk = A.fill + (cur.b0 + pt[0].x - data);
-          if (rx.hl && (!wbk || (wpend & 1u))) put_be16(pk + 10u, ip);
-          if (rx.fo && (!wbk || (wpend & 2u))) put_be16(pk + rx.fo, l4);
+          if (rx.hl) put_be16(pk + 10u, ip);
+          if (rx.fo) put_be16(pk + rx.fo, l4);
         }
       } else if (RX) {
         // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
@@ -2140,9 +2051,49 @@ __global__ __launch_bounds__(256, K == kSegDg || K == kSegDgW ? 3 : 1) void k_se
           v = le_to_be(pe - pt[0].p - (tx ? fsum : 0u), odd);
         }
         const uint64_t len = plen;
-        // (wbk: only a field wb_tile has not stored, if its last tile did not park)
-        uint8_t *pk = A.fill && (!wbk || wpend) ? A.fill + (cur.b0 + pt[0].x - data) : nullptr;
-        finish_packet(A, p, v, len, cur.sd, pk, (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
+        uint8_t *pk = A.fill ? A.fill + (cur.b0 + pt[0].x - data) : nullptr;
+        if (tx && wbk && park && fld + 2u <= len) {
+          // the field's offset in the parked (last) tile, wrapping below it;
+          // its line is stored whole below when the field lies in one line of
+          // this tile that holds no byte outside this chunk
+          wq = pt[0].x + fld - tb;
+          wf = true;
+          const Pos ls = wq & ~(Pos)127;
+          // (wq wraps for a field in an earlier tile: wq <= T - 2 keeps those out,
+          // a field ending right at this tile's start included)
+          if (wq <= T - 2u && (wq & 127u) != 127u && tb + ls >= x0 && tb + ls + 128u <= cur.xe) {
+            wl = (uint32_t)wq >> 7;
+            pk = nullptr;  // no 2-byte store
+          }
+        }
+        const uint32_t r = packet_value(A, v, len, cur.sd);
+        if (A.out) A.out[p] = (uint16_t)r;
+        wr = r;
+        if (pk) store_field(A, r, pk, (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
+      }
+    }
+    if (tx && wbk && park) {  // wave-uniform: the in-place write-back
+      // 1. Every field byte that lies in the tile goes into its parked copy, the
+      //    ones left to their 2-byte stores too (same bytes: a line stored whole
+      //    that holds one stays right).
+      uint8_t *sb = (uint8_t *)s_data[wid];
+      if (wf && wq < T) sb[wq] = (uint8_t)(wr >> 8);
+      if (wf && wq + 1u < T) sb[wq + 1u] = (uint8_t)wr;  // (wq + 1 == 0: a field from the tile before)
+      // 2. The lines holding a field of their own, as a 64-bit mask (T / 128 <= 64 lines).
+      const uint64_t m = (uint64_t)wave_or(wl < 32u ? 1u << wl : 0u) |
+                         ((uint64_t)wave_or(wl >= 32u && wl < 64u ? 1u << (wl - 32u) : 0u) << 32);
+      wave_lds_fence();
+      // 3. Those lines from the tile copy, as full-line 16-byte stores (8 lanes
+      //    per line, one contiguous KiB per instruction), non-temporal. Memory
+      //    then sees whole lines, not one partial write per field.
+      const __amdgpu_buffer_rsrc_t wr_r = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(A.fill + (cur.b0 + tb - data)), (short)0, (int)T, 0x00020000);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t k = (uint32_t)u * 64u + lane;
+        const uint4 d = s_data[wid][k];
+        const uint32_t off = ((m >> (k >> 3)) & 1u) ? 16u * k : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{d.x, d.y, d.z, d.w}, wr_r, (int)off, 0, 2);  // nt
       }
     }
     if ((ch + nwave) * CH >= A.n) return true;
@@ -2359,8 +2310,6 @@ const Variant kSegTx8c16 = YU_SEG16(8, kSegTx, "k_seg<8,tx,c16>");
 const Variant kSegTxW4 = YU_SEG(4, kSegTxW, "k_seg<4,txw>");
 const Variant kSegTxW8 = YU_SEG(8, kSegTxW, "k_seg<8,txw>");
 const Variant kSegTxW8c16 = YU_SEG16(8, kSegTxW, "k_seg<8,txw,c16>");
-const Variant kSegDgW8 = YU_SEG(8, kSegDgW, "k_seg<8,dgw>");
-const Variant kSegDgW8c16 = YU_SEG16(8, kSegDgW, "k_seg<8,dgw,c16>");
 const Variant kSegRx8c16 = YU_SEG16(8, kSegRx, "k_seg<8,rx,c16>");
 // (no 4 KiB-tile DG kind: datagram batches take the ragged picks, 8 KiB)
 const Variant kSegDg8 = YU_SEG(8, kSegDg, "k_seg<8,dg>");
@@ -2625,17 +2574,14 @@ int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
   return YU_OK;
 }
 
-// Ragged in place: the TX and DG kinds of k_seg take their TXW / DGW forms (the
-// whole-line write-back; 1M UDP datagrams U{40..200}: 67.5 -> 48.9 us) unless
-// YU_FILL_WB=0.
+// Ragged in place: the TX kinds of k_seg take their TXW form (the whole-line
+// write-back, 1M UDP datagrams U{40..200}: 62.3 -> 48.1 us) unless YU_FILL_WB=0.
 const Variant &pick_ragged_fill(int mode, uint64_t n, bool fill) {
   const Variant &v = pick_ragged(mode, n);
   if (!fill || !fill_wb()) return v;
   if (&v == &kSegTx8) return kSegTxW8;
   if (&v == &kSegTx8c16) return kSegTxW8c16;
   if (&v == &kSegTx4) return kSegTxW4;
-  if (&v == &kSegDg8) return kSegDgW8;
-  if (&v == &kSegDg8c16) return kSegDgW8c16;
   return v;
 }
 
