@@ -61,7 +61,9 @@
 //   k_seg<U, NT, K, CH>: ragged batches of more than 4096 packets, VERIFY_RX,
 //     and dense uniform packets of other sizes: a segmented sum over the byte
 //     stream of CH consecutive packets per wave (64, or 16 below 64K packets),
-//     U KiB tiles, packet sums as prefix differences (config 4, tun RX).
+//     U KiB tiles, packet sums as prefix differences (config 4, tun RX). Its
+//     TXW kind writes ragged TX batches in place, storing the fields of each
+//     chunk's last tile as whole 128-byte lines.
 //   k_hdr<NT>: the IPv4 header-only modes (<= 60 bytes of each packet), uniform
 //     and ragged: one lane per packet, 32-byte reads.
 //   k_loop<U, BE> / k_loop_rx<U>: one wave per packet, for ragged bursts of up
@@ -2575,7 +2577,8 @@ int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
 }
 
 // Ragged in place: the TX kinds of k_seg take their TXW form (the whole-line
-// write-back, 1M UDP datagrams U{40..200}: 62.3 -> 48.1 us) unless YU_FILL_WB=0.
+// write-back, 1M UDP datagrams U{40..200}: 67.5 -> 48.9 us, kbench 8, DESIGN.md
+// §5.4) unless YU_FILL_WB=0.
 const Variant &pick_ragged_fill(int mode, uint64_t n, bool fill) {
   const Variant &v = pick_ragged(mode, n);
   if (!fill || !fill_wb()) return v;
