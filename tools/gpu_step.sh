@@ -1,11 +1,10 @@
-# round 4, call I: closing evidence on the final tree -- the driver's three steps
-# (GPU suite, smoke, default bench line), the bench at the driver's settings, and a
-# rocprofv3 trace + PMC pass of every bench config
+# round 4, call J: the rest of the closing profiles (trace + PMC of configs 6, 7, 9,
+# 10, 11, 12, 13), and the fill / fuzz tests with the ragged kernels forced to 4 KiB
+# tiles (YU_RAGGED=seg4: the TXW kind's k_seg<4,txw> form)
 set -o pipefail
 mkdir -p gpurun_out
 T=r04i
-bash tools/verify_round.sh $T || exit 1
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${T}_driver.json 2> gpurun_out/bench_${T}_driver.err || { tail gpurun_out/bench_${T}_driver.err; exit 1; }
-python -c "import json;d=json.load(open('gpurun_out/bench_${T}_driver.json'));print(d['value'],d['roofline']['frac']);[print(k,v['kernel_avg_us'],v['roofline_frac'],v['kernel']) for k,v in d['other_configs'].items()]"
-CFGS="${CFGS:-3 2 8 4}" timeout -k 10 700 bash tools/profile.sh $T || exit 1
+YU_RAGGED=seg4 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "fill or fuzz or kernel_verified" --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_${T}_seg4.log 2>&1 || { tail -40 gpurun_out/gpu_tests_${T}_seg4.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_${T}_seg4.log
+CFGS="6 7 9 10 11 12 13" timeout -k 10 1000 bash tools/profile.sh $T || exit 1
 echo ok
