@@ -1,10 +1,11 @@
-# round 4, call J: the rest of the closing profiles (trace + PMC of configs 6, 7, 9,
-# 10, 11, 12, 13), and the fill / fuzz tests with the ragged kernels forced to 4 KiB
-# tiles (YU_RAGGED=seg4: the TXW kind's k_seg<4,txw> form)
+# round 4, call K: load policy of the ragged in-place writers -- plain loads
+# (YU_NT=0: the field's line more often still cached when its store arrives) against
+# the default non-temporal k_seg loads, for TX_DATAGRAM in place (kbench 15), TCP
+# segments U{64..1500} (7) and small UDP datagrams (8, the TXW kind)
 set -o pipefail
 mkdir -p gpurun_out
-T=r04i
-YU_RAGGED=seg4 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "fill or fuzz or kernel_verified" --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_${T}_seg4.log 2>&1 || { tail -40 gpurun_out/gpu_tests_${T}_seg4.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_${T}_seg4.log
-CFGS="6 7 9 10 11 12 13" timeout -k 10 1000 bash tools/profile.sh $T || exit 1
+F="KB_FILL=1 KB_ALIGN4=1"
+timeout -k 10 900 bash tools/ab.sh "15 $F" "15 $F YU_NT=0" "15 $F" "15 $F YU_NT=0" "7 $F" "7 $F YU_NT=0" "7 $F" "7 $F YU_NT=0" \
+  "8 $F" "8 $F YU_NT=0" "8 $F" "8 $F YU_NT=0" "15" "15 YU_NT=0" > gpurun_out/kbench_ab_r04k_fill_nt.log 2>&1 || { tail gpurun_out/kbench_ab_r04k_fill_nt.log; exit 1; }
+grep -E "^==|round" gpurun_out/kbench_ab_r04k_fill_nt.log
 echo ok

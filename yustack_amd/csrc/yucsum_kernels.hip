@@ -2557,6 +2557,11 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   a.small_waves = (uint32_t)cu_count(dev) * 4u * (uint32_t)seg_small_blocks();
   KernelFn k = A.fill && v.fill ? v.fill : v.fn[use_nt()];
   if (v.run && !runs) k = v.inter[A.fill ? fill_nt() : use_nt()];
+  // TX_DATAGRAM in place loads plainly too (fill_nt): a datagram's header line is
+  // then more often still cached when its two field stores arrive (1M datagrams
+  // U{40..1500}: 211.5 -> 203.1 us; the TXW kind is better off non-temporal, 48.7
+  // vs 52.1 us; profiles/r04/kbench_ab_r04k_fill_nt.log)
+  if (A.fill && (&v == &kSegDg8 || &v == &kSegDg8c16)) k = v.fn[fill_nt()];
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
