@@ -1755,8 +1755,6 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   // P(field end) - P(field start) without two more point evaluations per tile
   Pos fx = 0;
   uint32_t fk = 0, fsum = 0;
-  // DG in place: the fields already stored (bit 0: IPv4, bit 1: transport)
-  uint32_t dgdone = 0u;
   bool exact = false;
   uint32_t carry_l = 0, carry_t = 0;
   typename std::conditional<TXW, uint32_t, uint64_t>::type plen = 0;  // this lane's packet length
@@ -1791,7 +1789,6 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
 #pragma unroll
     for (int i = 0; i < NP; ++i) pt[i].p = pt[i].t = 0u;
     exact = K == kSegPlain && mode == YU_MODE_RAW && __any((int)(len > kLEMax));
-    dgdone = 0u;
     carry_l = carry_t = 0u;
   };
   begin_chunk(cur, ch * CH);
@@ -1941,28 +1938,6 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
           fx = split ? fx + 1u : kNoPt;
         }
       }
-      if (DG && A.fill) {
-        // In place: store a field as soon as every sum its value needs is known
-        // (a point in this tile or an earlier one; one at the tile's very end waits
-        // for its carry), while the datagram's header line, loaded plainly, is
-        // probably still in L2: a 2-byte store that hits a resident line is
-        // merged there instead of costing the memory side a partial write. The
-        // chunk's end stores the rest; c16 datagrams ending at the next lane's
-        // start wait for it too.
-        const Pos lim = tb + T;
-        const uint32_t odd = (uint32_t)pt[0].x & 1u;
-        uint8_t *pk = A.fill + (cur.b0 + pt[0].x - data);
-        const bool h_ok = rx.hl && (rx.h20 || pt[2].x < lim);
-        const uint32_t p2 = rx.h20 ? pt[0].p + rx.hsum : pt[2].p;  // P(header end)
-        if (h_ok && !(dgdone & 1u)) {
-          put_be16(pk + 10u, ~fold32(le_to_be(p2 - pt[0].p - rx.ipf, odd)) & 0xFFFFu);
-          dgdone |= 1u;
-        }
-        if (h_ok && rx.fo && !rx.tnext && pt[3].x < lim && fk == 0u && !(dgdone & 2u)) {
-          put_be16(pk + rx.fo, ~fold32(le_to_be(pt[3].p - p2 - fsum, odd) + rx.pseudo) & 0xFFFFu);
-          dgdone |= 2u;
-        }
-      }
       if (RX && !DG && parsed) {
         // A header straddling two tiles is parsed in the second, but a header
         // or total length under 20 bytes (IsValid accepts IHL 0..4) can put
@@ -2047,10 +2022,10 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
             A.out[2u * p + 1u] = (uint16_t)l4;
           }
         }
-        if (A.fill) {  // the fields not stored early (above)
+        if (A.fill) {
           uint8_t *pk = A.fill + (cur.b0 + pt[0].x - data);
-          if (rx.hl && !(dgdone & 1u)) put_be16(pk + 10u, ip);
-          if (rx.fo && !(dgdone & 2u)) put_be16(pk + rx.fo, l4);
+          if (rx.hl) put_be16(pk + 10u, ip);
+          if (rx.fo) put_be16(pk + rx.fo, l4);
         }
       } else if (RX) {
         // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
