@@ -1,11 +1,14 @@
-# round 4, call K: load policy of the ragged in-place writers -- plain loads
-# (YU_NT=0: the field's line more often still cached when its store arrives) against
-# the default non-temporal k_seg loads, for TX_DATAGRAM in place (kbench 15), TCP
-# segments U{64..1500} (7) and small UDP datagrams (8, the TXW kind)
+# round 4, call N: the whole GPU suite with each ragged measurement override forced
+# (parity only: every ragged kernel the selection can be forced onto, the TXW kind
+# included), then a longer seeded fuzz campaign on the final tree
 set -o pipefail
-mkdir -p gpurun_out
-F="KB_FILL=1 KB_ALIGN4=1"
-timeout -k 10 900 bash tools/ab.sh "15 $F" "15 $F YU_NT=0" "15 $F" "15 $F YU_NT=0" "7 $F" "7 $F YU_NT=0" "7 $F" "7 $F YU_NT=0" \
-  "8 $F" "8 $F YU_NT=0" "8 $F" "8 $F YU_NT=0" "15" "15 YU_NT=0" > gpurun_out/kbench_ab_r04k_fill_nt.log 2>&1 || { tail gpurun_out/kbench_ab_r04k_fill_nt.log; exit 1; }
-grep -E "^==|round" gpurun_out/kbench_ab_r04k_fill_nt.log
+mkdir -p gpurun_out/forced gpurun_out/fuzz
+for f in seg4 seg16 loop rag; do
+  YU_RAGGED=$f timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > gpurun_out/forced/gpu_tests_r04n_$f.log 2>&1 || { tail -40 gpurun_out/forced/gpu_tests_r04n_$f.log; exit 1; }
+  echo "$f: $(tail -1 gpurun_out/forced/gpu_tests_r04n_$f.log)"
+done
+run() { name=$1; shift; env "$@" timeout -k 10 500 python -u -m pytest -x -v --timeout 480 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "$name" > gpurun_out/fuzz/${name}_r04n.log 2>&1 || { tail -30 gpurun_out/fuzz/${name}_r04n.log; exit 1; }; tail -1 gpurun_out/fuzz/${name}_r04n.log; }
+run test_verify_rx_fuzz YU_RX_FUZZ_ITERS=600 YU_RX_FUZZ_SEED=9501 && \
+run test_tx_datagram_fuzz YU_TX_FUZZ_ITERS=600 YU_TX_FUZZ_SEED=9502 && \
+run test_random_batches_fuzz YU_FUZZ_ITERS=12000 YU_FUZZ_SEED=9503 YU_FUZZ_NBIG=70000 || exit 1
 echo ok
