@@ -386,7 +386,7 @@ def end_to_end(w: Workload, reps: int = 3):
         res[f"tx_burst{bn}_pinned_us_per_call"] = round((time.perf_counter() - t0) / k * 1e6, 1)
     ndev = torch.cuda.device_count()
     if ndev > 1:  # yu_csum_batch_host_uniform_multi: one shard per visible GPU, each on its own PCIe link
-        res.update(host_multi(w, list(range(ndev)), pinned, out))
+        res.update(host_multi_isolated(w.cfg, list(range(ndev))))
     return res
 
 
@@ -418,6 +418,45 @@ def host_multi(w: Workload, devs: list, pinned=None, want=None, reps: int = 3) -
     except Exception as e:  # reported, never fatal to the bench line
         res[f"pinned_{nd}gpu_error"] = str(e)[:200]
     return res
+
+
+# wall seconds for the --host-multi child (torch import, its own workload, 1 + reps passes)
+HOST_MULTI_TIMEOUT_S = float(os.environ.get("YU_BENCH_HOST_MULTI_TIMEOUT", "240"))
+
+
+def host_multi_isolated(config: int, devs: list, timeout: float = None) -> dict:
+    """host_multi in a child process (`bench.py --host-multi 0,1,...`), so that the
+    line survives whatever the multi-device host path does on a node it has not run
+    on before: a crash or a hang there costs the child and is reported as
+    pinned_<n>gpu_error, never the bench line. The child builds its own copy of the
+    workload (same config and seed as rank 0) and checks its result against the
+    device path itself. Started as a child (fork + exec of a fresh interpreter),
+    never by replacing this process."""
+    nd = len(devs)
+    timeout = HOST_MULTI_TIMEOUT_S if timeout is None else timeout
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                        "ROLE_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--config", str(config),
+           "--host-multi", ",".join(str(d) for d in devs)]
+    try:
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    except OSError as e:
+        return {f"pinned_{nd}gpu_error": f"child not started: {e}"[:200]}
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.communicate()
+        return {f"pinned_{nd}gpu_error": f"child killed after {timeout:.0f} s"}
+    for line in reversed(out.strip().splitlines()):
+        if line.startswith("{"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                break
+    tail = (err.strip().splitlines() or [""])[-1]
+    return {f"pinned_{nd}gpu_error": f"child exited {p.returncode}: {tail}"[:200]}
 
 
 def cpu_model() -> str:
@@ -673,7 +712,18 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end measurement")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, rendezvous, print their placement; no GPU work")
+    ap.add_argument("--host-multi", metavar="DEVS", default=None,
+                    help="(child of the bench) host memory over the listed GPUs, e.g. 0,1,2,3; "
+                         "prints one JSON object")
     args = ap.parse_args()
+
+    if args.host_multi is not None:
+        _imports()
+        devs = [int(d) for d in args.host_multi.split(",") if d.strip()]
+        torch.cuda.set_device(devs[0])
+        w = Workload(args.config, torch.device("cuda", devs[0]), seed=1000)
+        print(json.dumps(host_multi(w, devs)), flush=True)
+        return
 
     plan = resolve_launch(args.gpus, os.environ, _device_count())
     if plan["role"] == "spawn":
@@ -799,8 +849,9 @@ def rank_main(args, plan: dict) -> None:
         # is torn down: a rank waiting in an RCCL barrier meanwhile would keep a
         # collective kernel spinning on its GPU. The other ranks have left the timed
         # work and hold no kernels; they exit while this runs.
-        res["end_to_end_host_memory"] = host_multi(w, list(range(world)))
-        res["end_to_end_host_memory"]["measured"] = "rank 0 after destroy_process_group; other ranks idle"
+        res["end_to_end_host_memory"] = host_multi_isolated(args.config, list(range(world)))
+        res["end_to_end_host_memory"]["measured"] = ("a child of rank 0 after destroy_process_group; "
+                                                     "other ranks idle")
     if rank == 0:
         print(json.dumps(res), flush=True)
 

@@ -202,3 +202,13 @@ def test_rank_ignoring_sigterm_is_killed_after_grace():
     pids = _rank_pids(p, 2)
     assert p.wait(60) == 3  # the first failure's status
     assert not any(_alive(x) for x in pids)
+
+
+def test_host_multi_child_failure_is_reported_not_fatal():
+    """The multi-GPU host measurement runs in a child (`--host-multi`): a child that
+    cannot run (here: no GPU) or outlives its limit leaves an error entry, and the
+    caller — the bench line — carries on."""
+    r = bench.host_multi_isolated(3, [0, 1], timeout=300)
+    assert list(r) == ["pinned_2gpu_error"] and "child exited" in r["pinned_2gpu_error"], r
+    r = bench.host_multi_isolated(3, [0, 1], timeout=0.05)
+    assert r == {"pinned_2gpu_error": "child killed after 0 s"}, r

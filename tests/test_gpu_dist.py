@@ -167,6 +167,18 @@ def test_bench_self_launch_eight_ranks_on_one_card(dev):
     assert wall < 300
 
 
+def test_host_multi_child_on_one_card(dev):
+    """bench.host_multi_isolated, the form the line takes the host-memory rate over
+    several GPUs in (a child process, so a fault there cannot cost the line): two
+    shards both on device 0, bit-exact against the device path; a device that does
+    not exist comes back as an error entry."""
+    import bench
+    r = bench.host_multi_isolated(3, [0, 0])
+    assert r.get("pinned_2gpu_matches") is True and r["pinned_2gpu_GiB_s"] > 0, r
+    r = bench.host_multi_isolated(3, [0, 64])
+    assert "pinned_2gpu_error" in r and "pinned_2gpu_matches" not in r, r
+
+
 def test_launcher_device_count_matches_hip(dev):
     """bench._device_count (KFD topology + render nodes, no HIP) against
     torch.cuda.device_count() in a fresh process, with and without a visibility list."""

@@ -1744,11 +1744,6 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   // zero mask: give it a defined value once, not per chunk.
 #pragma unroll
   for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
-  // A header window that starts 4-aligned and crosses two tiles never gathers
-  // h[5] (its bytes lie past the 20-byte header), yet rx_parse reads it under a
-  // zero mask: give it a defined value once, not per chunk.
-#pragma unroll
-  for (int j = 0; j < 6; ++j) rx.h[j] = 0u;
   // TX, DG: the checksum field's next unread byte (kNoPt: none or done; DG: the
   // transport field), the bytes of it still to read (2, or 1 when the field
   // straddles two tiles) and the address-ordered LE sum of those read:
