@@ -421,7 +421,7 @@ def host_multi(w: Workload, devs: list, pinned=None, want=None, reps: int = 3) -
 
 
 # wall seconds for the --host-multi child (torch import, its own workload, 1 + reps passes)
-HOST_MULTI_TIMEOUT_S = float(os.environ.get("YU_BENCH_HOST_MULTI_TIMEOUT", "240"))
+HOST_MULTI_TIMEOUT_S = float(os.environ.get("YU_BENCH_HOST_MULTI_TIMEOUT", "180"))
 
 
 def host_multi_isolated(config: int, devs: list, timeout: float = None) -> dict:
