@@ -49,8 +49,10 @@ static std::vector<uint8_t> tcp_packet(const std::vector<uint8_t> &payload, uint
                                        uint16_t rcvWnd, const std::vector<uint8_t> &opts = {}) {
   std::vector<uint8_t> buf(header::TCPMinimumSize + header::IPv4MinimumSize + opts.size() +
                            payload.size());
-  memcpy(buf.data() + buf.size() - payload.size(), payload.data(), payload.size());
-  memcpy(buf.data() + buf.size() - payload.size() - opts.size(), opts.data(), opts.size());
+  if (!payload.empty())
+    memcpy(buf.data() + buf.size() - payload.size(), payload.data(), payload.size());
+  if (!opts.empty())
+    memcpy(buf.data() + buf.size() - payload.size() - opts.size(), opts.data(), opts.size());
   header::IPv4 ip{buf.data()};
   ip.Encode(header::IPv4MinimumSize, (uint16_t)buf.size(), 6, kTestAddr, kStackAddr);
   ip.SetChecksum((uint16_t)~ip.CalculateChecksum());
@@ -72,7 +74,7 @@ static std::vector<uint8_t> udp_packet(const std::vector<uint8_t> &payload, uint
                                        uint16_t dstPort) {
   const std::string testAddr("\x0a\x01\x00\x01", 4), stackAddr("\x0a\x01\x00\x02", 4);
   std::vector<uint8_t> buf(header::UDPMinimumSize + header::IPv4MinimumSize + payload.size());
-  memcpy(buf.data() + buf.size() - payload.size(), payload.data(), payload.size());
+  if (!payload.empty()) memcpy(buf.data() + buf.size() - payload.size(), payload.data(), payload.size());
   header::IPv4 ip{buf.data()};
   ip.Encode(header::IPv4MinimumSize, (uint16_t)buf.size(), 17, testAddr, stackAddr);
   ip.SetChecksum((uint16_t)~ip.CalculateChecksum());
