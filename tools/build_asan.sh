@@ -9,7 +9,7 @@ cd "$(dirname "$0")/.."
 mkdir -p tests/cpp/build
 /opt/rocm/bin/hipcc -O1 -g -std=c++17 --offload-arch=gfx950 \
   -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer \
-  -Iinclude -Iyustack_amd/csrc \
+  -DYU_TEST_QUICK_EXIT -Iinclude -Iyustack_amd/csrc \
   tests/cpp/test_checksum.cpp yustack_amd/csrc/yucsum_host.cpp yustack_amd/csrc/yucsum_scalar.cpp \
   yustack_amd/csrc/yucsum_kernels.hip \
   -Loracle/build -lcsum_oracle -Wl,-rpath,'$ORIGIN/../../../oracle/build' \
