@@ -269,6 +269,32 @@ static void test_gpu_batches() {
   batch::FillHostRagged(dblank.data(), off.data(), n, batch::TX_DATAGRAM, nullptr);
   EXPECT(dblank == blob, "host TX_DATAGRAM fill restores both fields of every datagram");
 
+  // past the direct path's 4 MiB: the sliced pipeline (staging slots, H2D, kernel,
+  // D2H per slice) from pageable memory, uniform and ragged, one device and three
+  {
+    const uint64_t bn = 12000, L = 1500;  // 18 MB
+    std::vector<uint8_t> big(bn * L);
+    for (auto &b : big) b = (uint8_t)rng();
+    std::vector<uint16_t> bo(bn, 0xAAAA), want(bn);
+    for (uint64_t i = 0; i < bn; ++i) want[i] = checksum::Checksum(big.data() + i * L, L, 0x4321);
+    batch::Side si;
+    si.initial = 0x4321;
+    batch::HostUniform(big.data(), L, (uint32_t)L, bn, batch::RAW, bo.data(), si);
+    EXPECT(bo == want, "host uniform pipelined (18 MB)");
+    std::fill(bo.begin(), bo.end(), 0xAAAA);
+    batch::HostUniform(big.data(), L, (uint32_t)L, bn, batch::RAW, bo.data(), si, {0, 0, 0});
+    EXPECT(bo == want, "host uniform pipelined, three shards");
+    std::vector<uint64_t> ro{0};
+    while (ro.back() < big.size()) ro.push_back(std::min<uint64_t>(big.size(), ro.back() + 40 + rng() % 2961));
+    const uint64_t rn = ro.size() - 1;
+    std::vector<uint16_t> ro_out(rn, 0xAAAA);
+    batch::HostRagged(big.data(), ro.data(), rn, batch::RAW, ro_out.data(), si);
+    bool same = true;
+    for (uint64_t i = 0; i < rn; ++i)
+      same &= ro_out[i] == checksum::Checksum(big.data() + ro[i], ro[i + 1] - ro[i], 0x4321);
+    EXPECT(same, "host ragged pipelined (18 MB, %lu packets)", rn);
+  }
+
   bool threw = false;
   try {
     batch::Uniform(d_segs, 16, 70000, 1, batch::TCP, d_out);
