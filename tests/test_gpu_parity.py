@@ -368,9 +368,11 @@ def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, shift):
         blob[offs[:-1].astype(np.int64) + 12] = 0x50
     addrs = _rand(rng, 8 * npk)
     want = oracle_c.batch(blob, mode, offsets=offs, addrs=addrs if mode != O.MODE_ICMP else None)
-    kind = "tx" if os.environ.get("YU_FILL_WB") == "0" else "txw"  # the write-back off: the TX kind
+    wb = os.environ.get("YU_FILL_WB", "1")
+    kind = "tx" if wb == "0" else "txw"  # the write-back off: the TX kind
+    big = f"k_seg<8,{kind},c56>" if wb == "2" else f"k_seg<8,{kind}>"  # 2: 56-packet chunks
     assert FORCED or batch.ragged_variant(mode, npk, fill=True) == (f"k_seg<8,{kind},c16>" if npk < 65536
-                                                                   else f"k_seg<8,{kind}>")
+                                                                   else big)
     pre = _rand(rng, shift)
     whole = _to(dev, np.concatenate([pre, blob]))
     d = whole[shift:]
