@@ -2312,6 +2312,12 @@ const Variant kSegTxW8c16 = YU_SEG16(8, kSegTxW, "k_seg<8,txw,c16>");
 const Variant kSegTxW8c56 = {"k_seg<8,txw,c56>", 0,
                              {k_seg<8, 0, kSegTxW, 56>, k_seg<8, 1, kSegTxW, 56>, k_seg<8, 1, kSegTxW, 56>},
                              64, 56};
+const Variant kSegTxW8c48 = {"k_seg<8,txw,c48>", 0,
+                             {k_seg<8, 0, kSegTxW, 48>, k_seg<8, 1, kSegTxW, 48>, k_seg<8, 1, kSegTxW, 48>},
+                             64, 48};
+const Variant kSegTxW8c60 = {"k_seg<8,txw,c60>", 0,
+                             {k_seg<8, 0, kSegTxW, 60>, k_seg<8, 1, kSegTxW, 60>, k_seg<8, 1, kSegTxW, 60>},
+                             64, 60};
 const Variant kSegRx8c16 = YU_SEG16(8, kSegRx, "k_seg<8,rx,c16>");
 // (no 4 KiB-tile DG kind: datagram batches take the ragged picks, 8 KiB)
 const Variant kSegDg8 = YU_SEG(8, kSegDg, "k_seg<8,dg>");
@@ -2506,7 +2512,7 @@ int fill_nt() {
 // field; 1 = the fields patched into the parked tile and their 128-byte lines
 // stored whole. YU_FILL_WB overrides.
 int fill_wb() {
-  static int v = env_int("YU_FILL_WB", 0, 2, 1);
+  static int v = env_int("YU_FILL_WB", 0, 4, 1);
   return v;
 }
 
@@ -2587,7 +2593,8 @@ int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
 const Variant &pick_ragged_fill(int mode, uint64_t n, bool fill) {
   const Variant &v = pick_ragged(mode, n);
   if (!fill || !fill_wb()) return v;
-  if (&v == &kSegTx8) return fill_wb() == 2 ? kSegTxW8c56 : kSegTxW8;
+  if (&v == &kSegTx8)
+    return fill_wb() == 2 ? kSegTxW8c56 : fill_wb() == 3 ? kSegTxW8c48 : fill_wb() == 4 ? kSegTxW8c60 : kSegTxW8;
   if (&v == &kSegTx8c16) return kSegTxW8c16;
   if (&v == &kSegTx4) return kSegTxW4;
   return v;
