@@ -370,7 +370,7 @@ def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, shift):
     want = oracle_c.batch(blob, mode, offsets=offs, addrs=addrs if mode != O.MODE_ICMP else None)
     wb = os.environ.get("YU_FILL_WB", "1")
     kind = "tx" if wb == "0" else "txw"  # the write-back off: the TX kind
-    ch = {"2": ",c56", "3": ",c48", "4": ",c60"}.get(wb, "")  # measurement chunk sizes
+    ch = {"2": ",c40", "3": ",c48", "4": ",c32"}.get(wb, "")  # measurement chunk sizes
     big = f"k_seg<8,{kind}{ch}>"
     assert FORCED or batch.ragged_variant(mode, npk, fill=True) == (f"k_seg<8,{kind},c16>" if npk < 65536
                                                                    else big)

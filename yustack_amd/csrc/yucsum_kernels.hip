@@ -2309,15 +2309,15 @@ const Variant kSegTxW8 = YU_SEG(8, kSegTxW, "k_seg<8,txw>");
 const Variant kSegTxW8c16 = YU_SEG16(8, kSegTxW, "k_seg<8,txw,c16>");
 // (measurement, YU_FILL_WB=2) 56-packet chunks: small datagrams' chunks then fit
 // one 8 KiB tile, so every field of the chunk lies in its parked last tile
-const Variant kSegTxW8c56 = {"k_seg<8,txw,c56>", 0,
-                             {k_seg<8, 0, kSegTxW, 56>, k_seg<8, 1, kSegTxW, 56>, k_seg<8, 1, kSegTxW, 56>},
-                             64, 56};
+const Variant kSegTxW8c40 = {"k_seg<8,txw,c40>", 0,
+                             {k_seg<8, 0, kSegTxW, 40>, k_seg<8, 1, kSegTxW, 40>, k_seg<8, 1, kSegTxW, 40>},
+                             64, 40};
 const Variant kSegTxW8c48 = {"k_seg<8,txw,c48>", 0,
                              {k_seg<8, 0, kSegTxW, 48>, k_seg<8, 1, kSegTxW, 48>, k_seg<8, 1, kSegTxW, 48>},
                              64, 48};
-const Variant kSegTxW8c60 = {"k_seg<8,txw,c60>", 0,
-                             {k_seg<8, 0, kSegTxW, 60>, k_seg<8, 1, kSegTxW, 60>, k_seg<8, 1, kSegTxW, 60>},
-                             64, 60};
+const Variant kSegTxW8c32 = {"k_seg<8,txw,c32>", 0,
+                             {k_seg<8, 0, kSegTxW, 32>, k_seg<8, 1, kSegTxW, 32>, k_seg<8, 1, kSegTxW, 32>},
+                             64, 32};
 const Variant kSegRx8c16 = YU_SEG16(8, kSegRx, "k_seg<8,rx,c16>");
 // (no 4 KiB-tile DG kind: datagram batches take the ragged picks, 8 KiB)
 const Variant kSegDg8 = YU_SEG(8, kSegDg, "k_seg<8,dg>");
@@ -2594,7 +2594,7 @@ const Variant &pick_ragged_fill(int mode, uint64_t n, bool fill) {
   const Variant &v = pick_ragged(mode, n);
   if (!fill || !fill_wb()) return v;
   if (&v == &kSegTx8)
-    return fill_wb() == 2 ? kSegTxW8c56 : fill_wb() == 3 ? kSegTxW8c48 : fill_wb() == 4 ? kSegTxW8c60 : kSegTxW8;
+    return fill_wb() == 2 ? kSegTxW8c40 : fill_wb() == 3 ? kSegTxW8c48 : fill_wb() == 4 ? kSegTxW8c32 : kSegTxW8;
   if (&v == &kSegTx8c16) return kSegTxW8c16;
   if (&v == &kSegTx4) return kSegTxW4;
   return v;
