@@ -15,7 +15,7 @@ from yustack_amd import batch
 
 # a measurement run that forces the ragged kernel (YU_RAGGED) checks parity only:
 # the default ragged kernel choice is not asserted then
-FORCED = bool(os.environ.get("YU_RAGGED"))
+FORCED = bool(os.environ.get("YU_RAGGED") or os.environ.get("YU_SEG_CH"))
 
 pytestmark = pytest.mark.gpu
 
@@ -368,12 +368,11 @@ def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, shift):
         blob[offs[:-1].astype(np.int64) + 12] = 0x50
     addrs = _rand(rng, 8 * npk)
     want = oracle_c.batch(blob, mode, offsets=offs, addrs=addrs if mode != O.MODE_ICMP else None)
-    wb = os.environ.get("YU_FILL_WB", "1")
-    kind = "tx" if wb == "0" else "txw"  # the write-back off: the TX kind
-    ch = {"2": ",c40", "3": ",c48", "4": ",c32"}.get(wb, "")  # measurement chunk sizes
+    kind = "tx" if os.environ.get("YU_FILL_WB") == "0" else "txw"  # the write-back off: the TX kind
+    ch = {"40": ",c40", "48": ",c48"}.get(os.environ.get("YU_SEG_CH", ""), "")  # measurement chunk sizes
     big = f"k_seg<8,{kind}{ch}>"
-    assert FORCED or batch.ragged_variant(mode, npk, fill=True) == (f"k_seg<8,{kind},c16>" if npk < 65536
-                                                                   else big)
+    assert bool(os.environ.get("YU_RAGGED")) or batch.ragged_variant(mode, npk, fill=True) == (
+        f"k_seg<8,{kind},c16>" if npk < 65536 else big)
     pre = _rand(rng, shift)
     whole = _to(dev, np.concatenate([pre, blob]))
     d = whole[shift:]

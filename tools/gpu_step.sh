@@ -1,27 +1,28 @@
-# round 4, call U: TXW chunk size sweep (measurement settings YU_FILL_WB=1..4:
-# 64, 40, 48, 32 packets per chunk) on small UDP (8) and mid-size TCP (7) fills,
-# plus parity of the fill tests at 48 and 60
+# round 4, call V: k_seg with 40- / 48-packet chunks for the 1M-packet picks
+# (YU_SEG_CH, measurement): the GPU suite with 40, then kbench over the ragged
+# shapes (4: U{64..9000}, 5: U{64..1500}, 15: TX_DATAGRAM, 16: small RX, 8/7 fills)
 set -o pipefail
 mkdir -p gpurun_out
-for wb in 2 4; do
-  YU_FILL_WB=$wb timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "fill_ragged or fuzz" > gpurun_out/gpu_tests_r04u_wb$wb.log 2>&1 || { tail -30 gpurun_out/gpu_tests_r04u_wb$wb.log; exit 1; }
-  tail -1 gpurun_out/gpu_tests_r04u_wb$wb.log
-done
+YU_SEG_CH=40 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_r04v_ch40.log 2>&1 || { tail -30 gpurun_out/gpu_tests_r04v_ch40.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_r04v_ch40.log
 hipcc -O2 -std=c++17 -Iinclude tools/kbench.cpp -Lyustack_amd -lyucsum -ldl -Wl,-rpath,$PWD/yustack_amd -o /tmp/kbench || exit 1
 for i in 1 2 3; do
-  for wb in 1 2 3 4; do
-    echo "== YU_FILL_WB=$wb"
-    YU_FILL_WB=$wb KB_FILL=1 KB_ALIGN4=1 timeout -k 10 120 /tmp/kbench 8 7 || exit 1
+  for ch in 0 40 48; do
+    echo "== YU_SEG_CH=$ch"
+    YU_SEG_CH=$ch timeout -k 10 200 /tmp/kbench 4 5 15 16 || exit 1
+    YU_SEG_CH=$ch KB_MODE=8 timeout -k 10 100 /tmp/kbench 15 || exit 1
+    YU_SEG_CH=$ch KB_FILL=1 KB_ALIGN4=1 timeout -k 10 100 /tmp/kbench 8 7 15 || exit 1
   done
-done > gpurun_out/kbench_ab_r04u_txw_chunk_sweep.log 2>&1
+done > gpurun_out/kbench_ab_r04v_seg_chunk.log 2>&1
 python3 - <<'PY'
 import re, collections
-d = collections.defaultdict(list); wb = None
-for l in open("gpurun_out/kbench_ab_r04u_txw_chunk_sweep.log"):
-    m = re.match(r"== YU_FILL_WB=(\d)", l)
-    if m: wb = m.group(1); continue
-    m = re.match(r"config(\d+) round \d+:\s+([\d.]+) us", l)
-    if m: d[(m.group(1), wb)].append(float(m.group(2)))
-for k in sorted(d): print(k, sorted(d[k]))
+d = collections.defaultdict(list); ch = None
+for l in open("gpurun_out/kbench_ab_r04v_seg_chunk.log"):
+    m = re.match(r"== YU_SEG_CH=(\d+)", l)
+    if m: ch = m.group(1); continue
+    m = re.match(r"config(\d+) round \d+:\s+([\d.]+) us.*\s(k_\S+)$", l.strip())
+    if m: d[(int(m.group(1)), m.group(3).split(',c')[0].rstrip('>'), ch)].append(float(m.group(2)))
+import statistics
+for k in sorted(d): print(k, "median", statistics.median(d[k]), sorted(d[k]))
 PY
 echo ok

@@ -2307,24 +2307,42 @@ const Variant kSegTx8c16 = YU_SEG16(8, kSegTx, "k_seg<8,tx,c16>");
 const Variant kSegTxW4 = YU_SEG(4, kSegTxW, "k_seg<4,txw>");
 const Variant kSegTxW8 = YU_SEG(8, kSegTxW, "k_seg<8,txw>");
 const Variant kSegTxW8c16 = YU_SEG16(8, kSegTxW, "k_seg<8,txw,c16>");
-// (measurement, YU_FILL_WB=2) 56-packet chunks: small datagrams' chunks then fit
-// one 8 KiB tile, so every field of the chunk lies in its parked last tile
-const Variant kSegTxW8c40 = {"k_seg<8,txw,c40>", 0,
-                             {k_seg<8, 0, kSegTxW, 40>, k_seg<8, 1, kSegTxW, 40>, k_seg<8, 1, kSegTxW, 40>},
-                             64, 40};
-const Variant kSegTxW8c48 = {"k_seg<8,txw,c48>", 0,
-                             {k_seg<8, 0, kSegTxW, 48>, k_seg<8, 1, kSegTxW, 48>, k_seg<8, 1, kSegTxW, 48>},
-                             64, 48};
-const Variant kSegTxW8c32 = {"k_seg<8,txw,c32>", 0,
-                             {k_seg<8, 0, kSegTxW, 32>, k_seg<8, 1, kSegTxW, 32>, k_seg<8, 1, kSegTxW, 32>},
-                             64, 32};
 const Variant kSegRx8c16 = YU_SEG16(8, kSegRx, "k_seg<8,rx,c16>");
 // (no 4 KiB-tile DG kind: datagram batches take the ragged picks, 8 KiB)
 const Variant kSegDg8 = YU_SEG(8, kSegDg, "k_seg<8,dg>");
 const Variant kSegDg8c16 = YU_SEG16(8, kSegDg, "k_seg<8,dg,c16>");
+// (measurement, YU_SEG_CH=40 / 48) the 1M-packet picks with 40- or 48-packet chunks
+#define YU_SEGC(U, K, CH, name) \
+  {name, 0, {k_seg<U, 0, K, CH>, k_seg<U, 1, K, CH>, k_seg<U, 1, K, CH>}, 64, CH}
+const Variant kSeg8c40 = YU_SEGC(8, kSegPlain, 40, "k_seg<8,c40>");
+const Variant kSegTx8c40 = YU_SEGC(8, kSegTx, 40, "k_seg<8,tx,c40>");
+const Variant kSegRx8c40 = YU_SEGC(8, kSegRx, 40, "k_seg<8,rx,c40>");
+const Variant kSegDg8c40 = YU_SEGC(8, kSegDg, 40, "k_seg<8,dg,c40>");
+const Variant kSegTxW8c40 = YU_SEGC(8, kSegTxW, 40, "k_seg<8,txw,c40>");
+const Variant kSeg8c48 = YU_SEGC(8, kSegPlain, 48, "k_seg<8,c48>");
+const Variant kSegTx8c48 = YU_SEGC(8, kSegTx, 48, "k_seg<8,tx,c48>");
+const Variant kSegRx8c48 = YU_SEGC(8, kSegRx, 48, "k_seg<8,rx,c48>");
+const Variant kSegDg8c48 = YU_SEGC(8, kSegDg, 48, "k_seg<8,dg,c48>");
+const Variant kSegTxW8c48 = YU_SEGC(8, kSegTxW, 48, "k_seg<8,txw,c48>");
+
+int seg_ch() {
+  static int v = [] {
+    const char *e = getenv("YU_SEG_CH");
+    const int c = e ? atoi(e) : 0;
+    return c == 40 || c == 48 ? c : 0;
+  }();
+  return v;
+}
 
 // The k_seg kind for a mode (not the IPv4 header-only modes).
 const Variant &seg_for(bool u8, int mode) {
+  if (u8 && seg_ch()) {
+    const bool c40 = seg_ch() == 40;
+    if (mode == YU_MODE_VERIFY_RX) return c40 ? kSegRx8c40 : kSegRx8c48;
+    if (mode == YU_MODE_TX_DATAGRAM) return c40 ? kSegDg8c40 : kSegDg8c48;
+    if (mode_is_tx(mode)) return c40 ? kSegTx8c40 : kSegTx8c48;
+    return c40 ? kSeg8c40 : kSeg8c48;
+  }
   if (mode == YU_MODE_VERIFY_RX) return u8 ? kSegRx8 : kSegRx4;
   if (mode == YU_MODE_TX_DATAGRAM) return kSegDg8;
   if (mode_is_tx(mode)) return u8 ? kSegTx8 : kSegTx4;
@@ -2512,7 +2530,7 @@ int fill_nt() {
 // field; 1 = the fields patched into the parked tile and their 128-byte lines
 // stored whole. YU_FILL_WB overrides.
 int fill_wb() {
-  static int v = env_int("YU_FILL_WB", 0, 4, 1);
+  static int v = env_int("YU_FILL_WB", 0, 1, 1);
   return v;
 }
 
@@ -2567,7 +2585,8 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   // then more often still cached when its two field stores arrive (1M datagrams
   // U{40..1500}: 211.5 -> 203.1 us; the TXW kind is better off non-temporal, 48.7
   // vs 52.1 us; profiles/r04/kbench_ab_r04k_fill_nt.log)
-  if (A.fill && (&v == &kSegDg8 || &v == &kSegDg8c16)) k = v.fn[fill_nt()];
+  if (A.fill && (&v == &kSegDg8 || &v == &kSegDg8c16 || &v == &kSegDg8c40 || &v == &kSegDg8c48))
+    k = v.fn[fill_nt()];
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
@@ -2593,8 +2612,9 @@ int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
 const Variant &pick_ragged_fill(int mode, uint64_t n, bool fill) {
   const Variant &v = pick_ragged(mode, n);
   if (!fill || !fill_wb()) return v;
-  if (&v == &kSegTx8)
-    return fill_wb() == 2 ? kSegTxW8c40 : fill_wb() == 3 ? kSegTxW8c48 : fill_wb() == 4 ? kSegTxW8c32 : kSegTxW8;
+  if (&v == &kSegTx8) return kSegTxW8;
+  if (&v == &kSegTx8c40) return kSegTxW8c40;
+  if (&v == &kSegTx8c48) return kSegTxW8c48;
   if (&v == &kSegTx8c16) return kSegTxW8c16;
   if (&v == &kSegTx4) return kSegTxW4;
   return v;
