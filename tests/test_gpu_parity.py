@@ -278,7 +278,7 @@ def test_verify_rx_fuzz(dev, oracle_c):
         got = batch.checksum_ragged(_to(dev, b), _to(dev, o.view(np.int64)), "verify_rx").cpu().numpy()
         want = oracle_c.batch(b, O.MODE_VERIFY_RX, offsets=o)
         assert np.array_equal(got, want), (it, npk, lo, hi, base_off, np.nonzero(got != want)[0][:10])
-    if int(os.environ.get("YU_RX_FUZZ_ITERS", "12")) >= len(sizes) and not os.environ.get("YU_RAGGED"):
+    if int(os.environ.get("YU_RX_FUZZ_ITERS", "12")) >= len(sizes) and not FORCED:
         assert {"k_loop<4,rx>", "k_seg<8,rx,c16>", "k_seg<8,rx>"} <= seen, seen
 
 
@@ -419,7 +419,7 @@ def test_tx_datagram_fuzz(dev, oracle_c):
         assert np.array_equal(got, want), (it, npk, "fill")
         filled = d.cpu().numpy()[pad:pad + blob.size]
         assert np.array_equal(filled, _tx_expected(blob, offs, want)[0]), (it, npk, "fill bytes")
-    if int(os.environ.get("YU_TX_FUZZ_ITERS", "12")) >= len(sizes) and not os.environ.get("YU_RAGGED"):
+    if int(os.environ.get("YU_TX_FUZZ_ITERS", "12")) >= len(sizes) and not FORCED:
         assert {"k_loop<4,dg>", "k_seg<8,dg,c16>", "k_seg<8,dg>"} <= seen, seen
 
 
