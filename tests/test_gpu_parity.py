@@ -15,7 +15,7 @@ from yustack_amd import batch
 
 # a measurement run that forces the ragged kernel (YU_RAGGED) checks parity only:
 # the default ragged kernel choice is not asserted then
-FORCED = bool(os.environ.get("YU_RAGGED") or os.environ.get("YU_SEG_CH"))
+FORCED = bool(os.environ.get("YU_RAGGED"))
 
 pytestmark = pytest.mark.gpu
 
@@ -368,11 +368,12 @@ def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, shift):
         blob[offs[:-1].astype(np.int64) + 12] = 0x50
     addrs = _rand(rng, 8 * npk)
     want = oracle_c.batch(blob, mode, offsets=offs, addrs=addrs if mode != O.MODE_ICMP else None)
-    kind = "tx" if os.environ.get("YU_FILL_WB") == "0" else "txw"  # the write-back off: the TX kind
-    ch = {"40": ",c40", "48": ",c48"}.get(os.environ.get("YU_SEG_CH", ""), "")  # measurement chunk sizes
-    big = f"k_seg<8,{kind}{ch}>"
-    assert bool(os.environ.get("YU_RAGGED")) or batch.ragged_variant(mode, npk, fill=True) == (
-        f"k_seg<8,{kind},c16>" if npk < 65536 else big)
+    # the write-back off (YU_FILL_WB=0): the TX kind; from 64K packets on the TXW kind
+    # takes 48-packet chunks
+    wb = os.environ.get("YU_FILL_WB") != "0"
+    big = "k_seg<8,txw,c48>" if wb else "k_seg<8,tx>"
+    assert FORCED or batch.ragged_variant(mode, npk, fill=True) == (
+        f"k_seg<8,{'txw' if wb else 'tx'},c16>" if npk < 65536 else big)
     pre = _rand(rng, shift)
     whole = _to(dev, np.concatenate([pre, blob]))
     d = whole[shift:]
@@ -406,6 +407,7 @@ def test_tx_datagram_fuzz(dev, oracle_c):
             lo, hi = min(lo, 100), min(hi, 300)
         blob, offs = rxgen.tx_batch(rng, npk, lo=lo, hi=hi, bad=float(rng.random()) * 0.5, pad4=True)
         seen.add(batch.ragged_variant("tx_datagram", npk))
+        seen.add("fill:" + batch.ragged_variant("tx_datagram", npk, fill=True))
         want = oracle_c.batch(blob, O.MODE_TX_DATAGRAM, offsets=offs)
         base_off = int(rng.integers(0, 16))
         b = np.concatenate([np.zeros(base_off, np.uint8), blob, np.zeros(32, np.uint8)])
@@ -420,7 +422,8 @@ def test_tx_datagram_fuzz(dev, oracle_c):
         filled = d.cpu().numpy()[pad:pad + blob.size]
         assert np.array_equal(filled, _tx_expected(blob, offs, want)[0]), (it, npk, "fill bytes")
     if int(os.environ.get("YU_TX_FUZZ_ITERS", "12")) >= len(sizes) and not FORCED:
-        assert {"k_loop<4,dg>", "k_seg<8,dg,c16>", "k_seg<8,dg>"} <= seen, seen
+        assert {"k_loop<4,dg>", "k_seg<8,dg,c16>", "k_seg<8,dg>", "fill:k_seg<8,dg,c16>",
+                "fill:k_seg<8,dg,c40>"} <= seen, seen
 
 
 @pytest.mark.parametrize("npk,kern", [(5000, "k_seg<8,dg,c16>"), (66000, "k_seg<8,dg>")])
@@ -442,6 +445,30 @@ def test_tx_datagram_header_straddles_tile(dev, oracle_c, npk, kern):
         want = oracle_c.batch(blob, O.MODE_TX_DATAGRAM, offsets=offs)
         assert np.array_equal(got, want), (base_off, np.nonzero(got != want)[0][:10])
         assert (want[0::2] != 0).mean() > 0.9  # in contract: fillers and specials alike
+
+
+@pytest.mark.parametrize("npk,kern", [(5000, "k_seg<8,dg,c16>"), (66000, "k_seg<8,dg,c40>")])
+def test_tx_datagram_fill_header_straddles_tile(dev, oracle_c, npk, kern):
+    """The same tile-straddling headers written in place: TX_DATAGRAM's fill takes
+    40-packet chunks from 64K datagrams on (16 below), so the batch is laid out on
+    that chunk's tile boundaries; values, both fields, and no other byte changed."""
+    import rxgen
+    assert FORCED or batch.ragged_variant("tx_datagram", npk, fill=True) == kern
+    chunk = 16 if "c16" in kern else 40
+    rng = np.random.default_rng(9650 + npk)
+    special = lambda r, total: rxgen.tx_packet(r, max(0, total - 20), ihl=5)  # noqa: E731
+    for base_off in (0, 3):
+        blob, offs = rxgen.tile_edge_batch(rng, npk, chunk, base_off, tile=8192, special=special)
+        for i in range(npk):
+            a, e = int(offs[i]), int(offs[i + 1])
+            blob[a:e] = np.frombuffer(bytes(rxgen.tcp_contract(bytearray(blob[a:e].tobytes()))), np.uint8)
+        want = oracle_c.batch(blob, O.MODE_TX_DATAGRAM, offsets=offs)
+        d = _to(dev, blob)
+        got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), "tx_datagram", fill=True).cpu().numpy()
+        assert np.array_equal(got, want), (base_off, np.nonzero(got != want)[0][:10])
+        exp = _tx_expected(blob, offs, want)[0]
+        bad = np.nonzero(d.cpu().numpy() != exp)[0]
+        assert bad.size == 0, (base_off, bad[:10])
 
 
 @pytest.mark.parametrize("npk", [777, 70000])

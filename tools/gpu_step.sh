@@ -1,28 +1,13 @@
-# round 4, call V: k_seg with 40- / 48-packet chunks for the 1M-packet picks
-# (YU_SEG_CH, measurement): the GPU suite with 40, then kbench over the ragged
-# shapes (4: U{64..9000}, 5: U{64..1500}, 15: TX_DATAGRAM, 16: small RX, 8/7 fills)
+# round 4, call W: in-place chunk sizes adopted (TXW 48, TX_DATAGRAM fill 40 packets
+# per chunk from 64K packets on): the GPU suite, smoke, the bench at the driver's
+# settings, a TXW / DG-fill fuzz campaign, and configs 12 / 13 re-profiled
 set -o pipefail
 mkdir -p gpurun_out
-YU_SEG_CH=40 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_r04v_ch40.log 2>&1 || { tail -30 gpurun_out/gpu_tests_r04v_ch40.log; exit 1; }
-tail -1 gpurun_out/gpu_tests_r04v_ch40.log
-hipcc -O2 -std=c++17 -Iinclude tools/kbench.cpp -Lyustack_amd -lyucsum -ldl -Wl,-rpath,$PWD/yustack_amd -o /tmp/kbench || exit 1
-for i in 1 2 3; do
-  for ch in 0 40 48; do
-    echo "== YU_SEG_CH=$ch"
-    YU_SEG_CH=$ch timeout -k 10 200 /tmp/kbench 4 5 15 16 || exit 1
-    YU_SEG_CH=$ch KB_MODE=8 timeout -k 10 100 /tmp/kbench 15 || exit 1
-    YU_SEG_CH=$ch KB_FILL=1 KB_ALIGN4=1 timeout -k 10 100 /tmp/kbench 8 7 15 || exit 1
-  done
-done > gpurun_out/kbench_ab_r04v_seg_chunk.log 2>&1
-python3 - <<'PY'
-import re, collections
-d = collections.defaultdict(list); ch = None
-for l in open("gpurun_out/kbench_ab_r04v_seg_chunk.log"):
-    m = re.match(r"== YU_SEG_CH=(\d+)", l)
-    if m: ch = m.group(1); continue
-    m = re.match(r"config(\d+) round \d+:\s+([\d.]+) us.*\s(k_\S+)$", l.strip())
-    if m: d[(int(m.group(1)), m.group(3).split(',c')[0].rstrip('>'), ch)].append(float(m.group(2)))
-import statistics
-for k in sorted(d): print(k, "median", statistics.median(d[k]), sorted(d[k]))
-PY
+bash tools/verify_round.sh r04w || exit 1
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_r04w_driver.json 2> gpurun_out/bench_r04w_driver.err || { tail gpurun_out/bench_r04w_driver.err; exit 1; }
+YU_TX_FUZZ_ITERS=300 YU_TX_FUZZ_SEED=9601 YU_FUZZ_ITERS=3000 YU_FUZZ_SEED=9602 YU_FUZZ_NBIG=70000 \
+  timeout -k 10 500 python -u -m pytest -x -q --timeout 480 --timeout-method thread tests/test_gpu_parity.py -m gpu \
+  -k "test_tx_datagram_fuzz or test_random_batches_fuzz" > gpurun_out/fuzz_r04w.log 2>&1 || { tail -30 gpurun_out/fuzz_r04w.log; exit 1; }
+tail -1 gpurun_out/fuzz_r04w.log
+CFGS="12 13" bash tools/profile.sh r04w || exit 1
 echo ok

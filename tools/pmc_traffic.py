@@ -33,7 +33,8 @@ def short_name(full):
         return f"k_loop<{args[0]},{'BE' if args[2] == 'true' else 'LE'}>"
     if k == "k_seg":
         kind = {"2": ",rx", "true": ",rx", "1": ",tx", "3": ",dg", "4": ",txw"}.get(args[2], "")  # template K
-        return f"k_seg<{args[0]}{kind}>"
+        ch = f",c{args[3]}" if len(args) > 3 and args[3] != "64" else ""  # packets per chunk
+        return f"k_seg<{args[0]}{kind}{ch}>"
     if k == "k_rag":
         return f"k_rag<{args[0]},{args[1]}>"
     return k

@@ -2305,44 +2305,24 @@ const Variant kSeg8c16 = YU_SEG16(8, kSegPlain, "k_seg<8,c16>");
 const Variant kSegTx8c16 = YU_SEG16(8, kSegTx, "k_seg<8,tx,c16>");
 // the TX kinds' in-place form for ragged batches (the whole-line write-back)
 const Variant kSegTxW4 = YU_SEG(4, kSegTxW, "k_seg<4,txw>");
-const Variant kSegTxW8 = YU_SEG(8, kSegTxW, "k_seg<8,txw>");
 const Variant kSegTxW8c16 = YU_SEG16(8, kSegTxW, "k_seg<8,txw,c16>");
 const Variant kSegRx8c16 = YU_SEG16(8, kSegRx, "k_seg<8,rx,c16>");
 // (no 4 KiB-tile DG kind: datagram batches take the ragged picks, 8 KiB)
 const Variant kSegDg8 = YU_SEG(8, kSegDg, "k_seg<8,dg>");
 const Variant kSegDg8c16 = YU_SEG16(8, kSegDg, "k_seg<8,dg,c16>");
-// (measurement, YU_SEG_CH=40 / 48) the 1M-packet picks with 40- or 48-packet chunks
+// In place, from 64K packets on: smaller chunks. The TXW kind at 48 packets (1M UDP
+// datagrams U{40..200}: 48.7 -> 46.3 us; U{64..1500} TCP 192.9 -> 190.4: a small
+// datagram chunk then fits one 8 KiB tile, so all its fields go out as whole
+// lines), TX_DATAGRAM at 40 (U{40..1500}: 204.3 -> 198.7 us). The read-only kinds
+// keep 64 (RX U{40..200} 26.5 vs 27.5 at 48 and 30.3 at 40; plain unchanged).
+// profiles/r04/kbench_ab_r04v_seg_chunk.log (and r04s/r04t/r04u for 32..60)
 #define YU_SEGC(U, K, CH, name) \
   {name, 0, {k_seg<U, 0, K, CH>, k_seg<U, 1, K, CH>, k_seg<U, 1, K, CH>}, 64, CH}
-const Variant kSeg8c40 = YU_SEGC(8, kSegPlain, 40, "k_seg<8,c40>");
-const Variant kSegTx8c40 = YU_SEGC(8, kSegTx, 40, "k_seg<8,tx,c40>");
-const Variant kSegRx8c40 = YU_SEGC(8, kSegRx, 40, "k_seg<8,rx,c40>");
-const Variant kSegDg8c40 = YU_SEGC(8, kSegDg, 40, "k_seg<8,dg,c40>");
-const Variant kSegTxW8c40 = YU_SEGC(8, kSegTxW, 40, "k_seg<8,txw,c40>");
-const Variant kSeg8c48 = YU_SEGC(8, kSegPlain, 48, "k_seg<8,c48>");
-const Variant kSegTx8c48 = YU_SEGC(8, kSegTx, 48, "k_seg<8,tx,c48>");
-const Variant kSegRx8c48 = YU_SEGC(8, kSegRx, 48, "k_seg<8,rx,c48>");
-const Variant kSegDg8c48 = YU_SEGC(8, kSegDg, 48, "k_seg<8,dg,c48>");
 const Variant kSegTxW8c48 = YU_SEGC(8, kSegTxW, 48, "k_seg<8,txw,c48>");
-
-int seg_ch() {
-  static int v = [] {
-    const char *e = getenv("YU_SEG_CH");
-    const int c = e ? atoi(e) : 0;
-    return c == 40 || c == 48 ? c : 0;
-  }();
-  return v;
-}
+const Variant kSegDg8c40 = YU_SEGC(8, kSegDg, 40, "k_seg<8,dg,c40>");
 
 // The k_seg kind for a mode (not the IPv4 header-only modes).
 const Variant &seg_for(bool u8, int mode) {
-  if (u8 && seg_ch()) {
-    const bool c40 = seg_ch() == 40;
-    if (mode == YU_MODE_VERIFY_RX) return c40 ? kSegRx8c40 : kSegRx8c48;
-    if (mode == YU_MODE_TX_DATAGRAM) return c40 ? kSegDg8c40 : kSegDg8c48;
-    if (mode_is_tx(mode)) return c40 ? kSegTx8c40 : kSegTx8c48;
-    return c40 ? kSeg8c40 : kSeg8c48;
-  }
   if (mode == YU_MODE_VERIFY_RX) return u8 ? kSegRx8 : kSegRx4;
   if (mode == YU_MODE_TX_DATAGRAM) return kSegDg8;
   if (mode_is_tx(mode)) return u8 ? kSegTx8 : kSegTx4;
@@ -2585,8 +2565,7 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   // then more often still cached when its two field stores arrive (1M datagrams
   // U{40..1500}: 211.5 -> 203.1 us; the TXW kind is better off non-temporal, 48.7
   // vs 52.1 us; profiles/r04/kbench_ab_r04k_fill_nt.log)
-  if (A.fill && (&v == &kSegDg8 || &v == &kSegDg8c16 || &v == &kSegDg8c40 || &v == &kSegDg8c48))
-    k = v.fn[fill_nt()];
+  if (A.fill && (&v == &kSegDg8 || &v == &kSegDg8c16 || &v == &kSegDg8c40)) k = v.fn[fill_nt()];
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
@@ -2611,10 +2590,9 @@ int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
 // §5.4) unless YU_FILL_WB=0.
 const Variant &pick_ragged_fill(int mode, uint64_t n, bool fill) {
   const Variant &v = pick_ragged(mode, n);
+  if (fill && &v == &kSegDg8) return kSegDg8c40;
   if (!fill || !fill_wb()) return v;
-  if (&v == &kSegTx8) return kSegTxW8;
-  if (&v == &kSegTx8c40) return kSegTxW8c40;
-  if (&v == &kSegTx8c48) return kSegTxW8c48;
+  if (&v == &kSegTx8) return kSegTxW8c48;
   if (&v == &kSegTx8c16) return kSegTxW8c16;
   if (&v == &kSegTx4) return kSegTxW4;
   return v;
