@@ -2320,6 +2320,13 @@ const Variant kSegDg8c16 = YU_SEG16(8, kSegDg, "k_seg<8,dg,c16>");
   {name, 0, {k_seg<U, 0, K, CH>, k_seg<U, 1, K, CH>, k_seg<U, 1, K, CH>}, 64, CH}
 const Variant kSegTxW8c48 = YU_SEGC(8, kSegTxW, 48, "k_seg<8,txw,c48>");
 const Variant kSegDg8c40 = YU_SEGC(8, kSegDg, 40, "k_seg<8,dg,c40>");
+// (measurement only, YU_DG_FILL_CH=32 / 24)
+const Variant kSegDg8c32 = YU_SEGC(8, kSegDg, 32, "k_seg<8,dg,c32>");
+const Variant kSegDg8c24 = YU_SEGC(8, kSegDg, 24, "k_seg<8,dg,c24>");
+int dg_fill_ch() {
+  static int v = env_int("YU_DG_FILL_CH", 24, 40, 40);
+  return v;
+}
 
 // The k_seg kind for a mode (not the IPv4 header-only modes).
 const Variant &seg_for(bool u8, int mode) {
@@ -2565,7 +2572,9 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   // then more often still cached when its two field stores arrive (1M datagrams
   // U{40..1500}: 211.5 -> 203.1 us; the TXW kind is better off non-temporal, 48.7
   // vs 52.1 us; profiles/r04/kbench_ab_r04k_fill_nt.log)
-  if (A.fill && (&v == &kSegDg8 || &v == &kSegDg8c16 || &v == &kSegDg8c40)) k = v.fn[fill_nt()];
+  if (A.fill && (&v == &kSegDg8 || &v == &kSegDg8c16 || &v == &kSegDg8c40 || &v == &kSegDg8c32 ||
+                 &v == &kSegDg8c24))
+    k = v.fn[fill_nt()];
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
 }
@@ -2590,7 +2599,8 @@ int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
 // §5.4) unless YU_FILL_WB=0.
 const Variant &pick_ragged_fill(int mode, uint64_t n, bool fill) {
   const Variant &v = pick_ragged(mode, n);
-  if (fill && &v == &kSegDg8) return kSegDg8c40;
+  if (fill && &v == &kSegDg8)
+    return dg_fill_ch() == 32 ? kSegDg8c32 : dg_fill_ch() == 24 ? kSegDg8c24 : kSegDg8c40;
   if (!fill || !fill_wb()) return v;
   if (&v == &kSegTx8) return kSegTxW8c48;
   if (&v == &kSegTx8c16) return kSegTxW8c16;
