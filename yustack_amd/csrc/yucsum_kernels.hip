@@ -2323,10 +2323,6 @@ const Variant kSegDg8c40 = YU_SEGC(8, kSegDg, 40, "k_seg<8,dg,c40>");
 // (measurement only, YU_DG_FILL_CH=32 / 24)
 const Variant kSegDg8c32 = YU_SEGC(8, kSegDg, 32, "k_seg<8,dg,c32>");
 const Variant kSegDg8c24 = YU_SEGC(8, kSegDg, 24, "k_seg<8,dg,c24>");
-int dg_fill_ch() {
-  static int v = env_int("YU_DG_FILL_CH", 24, 40, 40);
-  return v;
-}
 
 // The k_seg kind for a mode (not the IPv4 header-only modes).
 const Variant &seg_for(bool u8, int mode) {
@@ -2516,6 +2512,11 @@ int fill_nt() {
 // The ragged in-place writer of k_seg's TX kind (wbk): 0 = one 2-byte store per
 // field; 1 = the fields patched into the parked tile and their 128-byte lines
 // stored whole. YU_FILL_WB overrides.
+int dg_fill_ch() {
+  static int v = env_int("YU_DG_FILL_CH", 24, 40, 40);
+  return v;
+}
+
 int fill_wb() {
   static int v = env_int("YU_FILL_WB", 0, 1, 1);
   return v;
