@@ -11,9 +11,11 @@
  * compiled with -O2 -fno-tree-vectorize this is the "reference-faithful"
  * scalar baseline.
  *
- * Pinning: the reference is Go and no Go toolchain exists in this image, and
- * it ships no known-answer vectors. This oracle is pinned by
- * (1) known answers produced by EXECUTING the reference's own source
+ * PARITY UNPINNED (by the task's rule): the reference is Go, no Go toolchain
+ * exists in this image, and it ships no known-answer vectors,
+ * so neither the reference's fixtures nor the reference itself run here can
+ * pin this oracle. The evidence it rests on instead: (1) known answers
+ * produced by EXECUTING the reference's own source
  * (checksum/checksum.go, header/{ipv4,tcp,udp}.go) with a minimal Go-subset
  * interpreter, tests/golden/goexec.py -> tests/golden/refexec.json (every
  * batch mode, the Checksum/Combine/PseudoHeaderChecksum functions, the uint32
@@ -22,7 +24,9 @@
  * built as its test harnesses build them (transport/tcp/testing/context/
  * context.go:164-209, transport/udp/udp_test.go:105-144); and (4) an
  * independent Python twin (oracle/oracle.py) plus a closed form, all checked
- * in tests/test_oracle.py.
+ * in tests/test_oracle.py; (5) datagrams the Linux kernel verified or built
+ * (tests/golden/kernel_verified.npz). The interpreter in (1) is written for
+ * this repo, a stand-in for the absent Go toolchain, not the reference run.
  */
 #include <pthread.h>
 #include <stdint.h>

@@ -11,13 +11,16 @@ Two independent CPU restatements of yustack's checksum path
 Only ``tests/``, ``__graft_entry__.smoke()`` and bench.py's cpu_baseline leg may
 import this module. The product package ``yustack_amd`` never does.
 
-Pinning status: the reference is Go (no toolchain in this image)
-and ships no known-answer vectors. This oracle is pinned by known answers produced by
-executing the reference's own source (checksum/checksum.go, header/{ipv4,tcp,udp}.go)
-with the Go-subset interpreter tests/golden/goexec.py (tests/golden/refexec.json), by
-RFC 1071 §3's published example, by the reference's own test-side property
-(checker/checker.go:32-35,80-92) on packets built the way its test harnesses build
-them, and by agreement of the two independent restatements plus the closed form.
+PARITY UNPINNED (by the task's rule): the reference is Go (no
+toolchain in this image) and ships no known-answer vectors, so it cannot pin this
+oracle. The evidence it rests on instead: known answers produced by executing the
+reference's own source (checksum/checksum.go, header/{ipv4,tcp,udp}.go) with the
+Go-subset interpreter tests/golden/goexec.py (tests/golden/refexec.json; the
+interpreter is this repo's stand-in for the absent toolchain), RFC 1071 §3's published
+example, the reference's own test-side property (checker/checker.go:32-35,80-92) on
+packets built the way its test harnesses build them, agreement of the two independent
+restatements plus the closed form, and datagrams the Linux kernel verified or built
+(tests/golden/kernel_verified.npz).
 """
 from __future__ import annotations
 

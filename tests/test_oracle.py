@@ -1,10 +1,12 @@
-"""The oracle pinned before it is trusted (CPU only).
+"""The oracle checked before it is trusted (CPU only).
 
 The reference is Go and cannot run here, and ships no known-answer vectors
-(SURVEY.md §8c). The oracle is pinned by RFC 1071's published example, a published
-IPv4 header checksum, the reference's own checker property on packets built like
-its test harnesses, the closed form, and agreement of two independent
-restatements (C and Python) — all recorded in tests/golden/golden.json.
+(SURVEY.md §8c), so by the task's rule the oracle is parity unpinned.
+It is checked against RFC 1071's published example, a published IPv4 header
+checksum, the reference's own checker property on packets built like its test
+harnesses, the closed form, and agreement of two independent restatements (C and
+Python) — all recorded in tests/golden/golden.json — plus the known answers of
+tests/golden/refexec.json (the reference's source run by this repo's interpreter).
 """
 import json
 import os
