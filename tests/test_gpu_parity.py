@@ -16,6 +16,10 @@ from yustack_amd import batch
 # a measurement run that forces the ragged kernel (YU_RAGGED) checks parity only:
 # the default ragged kernel choice is not asserted then
 FORCED = bool(os.environ.get("YU_RAGGED"))
+# TX_DATAGRAM in place from 64K datagrams on: 40-packet chunks, or the measurement
+# setting YU_DG_FILL_CH (32 / 24)
+DG_FILL_CH = int(os.environ.get("YU_DG_FILL_CH", "40"))
+DG_FILL = f"k_seg<8,dg,c{DG_FILL_CH}>"
 
 pytestmark = pytest.mark.gpu
 
@@ -423,7 +427,7 @@ def test_tx_datagram_fuzz(dev, oracle_c):
         assert np.array_equal(filled, _tx_expected(blob, offs, want)[0]), (it, npk, "fill bytes")
     if int(os.environ.get("YU_TX_FUZZ_ITERS", "12")) >= len(sizes) and not FORCED:
         assert {"k_loop<4,dg>", "k_seg<8,dg,c16>", "k_seg<8,dg>", "fill:k_seg<8,dg,c16>",
-                "fill:k_seg<8,dg,c40>"} <= seen, seen
+                "fill:" + DG_FILL} <= seen, seen
 
 
 @pytest.mark.parametrize("npk,kern", [(5000, "k_seg<8,dg,c16>"), (66000, "k_seg<8,dg>")])
@@ -447,14 +451,14 @@ def test_tx_datagram_header_straddles_tile(dev, oracle_c, npk, kern):
         assert (want[0::2] != 0).mean() > 0.9  # in contract: fillers and specials alike
 
 
-@pytest.mark.parametrize("npk,kern", [(5000, "k_seg<8,dg,c16>"), (66000, "k_seg<8,dg,c40>")])
+@pytest.mark.parametrize("npk,kern", [(5000, "k_seg<8,dg,c16>"), (66000, DG_FILL)])
 def test_tx_datagram_fill_header_straddles_tile(dev, oracle_c, npk, kern):
     """The same tile-straddling headers written in place: TX_DATAGRAM's fill takes
     40-packet chunks from 64K datagrams on (16 below), so the batch is laid out on
     that chunk's tile boundaries; values, both fields, and no other byte changed."""
     import rxgen
     assert FORCED or batch.ragged_variant("tx_datagram", npk, fill=True) == kern
-    chunk = 16 if "c16" in kern else 40
+    chunk = 16 if "c16" in kern else DG_FILL_CH
     rng = np.random.default_rng(9650 + npk)
     special = lambda r, total: rxgen.tx_packet(r, max(0, total - 20), ihl=5)  # noqa: E731
     for base_off in (0, 3):
