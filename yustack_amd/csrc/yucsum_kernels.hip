@@ -2509,14 +2509,16 @@ int fill_nt() {
   return v;
 }
 
-// The ragged in-place writer of k_seg's TX kind (wbk): 0 = one 2-byte store per
-// field; 1 = the fields patched into the parked tile and their 128-byte lines
-// stored whole. YU_FILL_WB overrides.
+// Packets per chunk of TX_DATAGRAM in place from 64K datagrams on: 40; 32 and 24
+// are measurement settings (YU_DG_FILL_CH), no faster.
 int dg_fill_ch() {
   static int v = env_int("YU_DG_FILL_CH", 24, 40, 40);
   return v;
 }
 
+// The ragged in-place writer of k_seg's TX kind (wbk): 0 = one 2-byte store per
+// field; 1 = the fields patched into the parked tile and their 128-byte lines
+// stored whole. YU_FILL_WB overrides.
 int fill_wb() {
   static int v = env_int("YU_FILL_WB", 0, 1, 1);
   return v;
