@@ -16,9 +16,8 @@ from yustack_amd import batch
 # a measurement run that forces the ragged kernel (YU_RAGGED) checks parity only:
 # the default ragged kernel choice is not asserted then
 FORCED = bool(os.environ.get("YU_RAGGED"))
-# TX_DATAGRAM in place from 64K datagrams on: 40-packet chunks, or the measurement
-# setting YU_DG_FILL_CH (32 / 24)
-DG_FILL_CH = int(os.environ.get("YU_DG_FILL_CH", "40"))
+# TX_DATAGRAM in place from 64K datagrams on: 40-packet chunks
+DG_FILL_CH = 40
 DG_FILL = f"k_seg<8,dg,c{DG_FILL_CH}>"
 
 pytestmark = pytest.mark.gpu

@@ -2320,9 +2320,6 @@ const Variant kSegDg8c16 = YU_SEG16(8, kSegDg, "k_seg<8,dg,c16>");
   {name, 0, {k_seg<U, 0, K, CH>, k_seg<U, 1, K, CH>, k_seg<U, 1, K, CH>}, 64, CH}
 const Variant kSegTxW8c48 = YU_SEGC(8, kSegTxW, 48, "k_seg<8,txw,c48>");
 const Variant kSegDg8c40 = YU_SEGC(8, kSegDg, 40, "k_seg<8,dg,c40>");
-// (measurement only, YU_DG_FILL_CH=32 / 24)
-const Variant kSegDg8c32 = YU_SEGC(8, kSegDg, 32, "k_seg<8,dg,c32>");
-const Variant kSegDg8c24 = YU_SEGC(8, kSegDg, 24, "k_seg<8,dg,c24>");
 
 // The k_seg kind for a mode (not the IPv4 header-only modes).
 const Variant &seg_for(bool u8, int mode) {
@@ -2509,13 +2506,6 @@ int fill_nt() {
   return v;
 }
 
-// Packets per chunk of TX_DATAGRAM in place from 64K datagrams on: 40; 32 and 24
-// are measurement settings (YU_DG_FILL_CH), no faster.
-int dg_fill_ch() {
-  static int v = env_int("YU_DG_FILL_CH", 24, 40, 40);
-  return v;
-}
-
 // The ragged in-place writer of k_seg's TX kind (wbk): 0 = one 2-byte store per
 // field; 1 = the fields patched into the parked tile and their 128-byte lines
 // stored whole. YU_FILL_WB overrides.
@@ -2575,8 +2565,7 @@ int launch(const Variant &v, const BatchArgs &A, hipStream_t stream) {
   // then more often still cached when its two field stores arrive (1M datagrams
   // U{40..1500}: 211.5 -> 203.1 us; the TXW kind is better off non-temporal, 48.7
   // vs 52.1 us; profiles/r04/kbench_ab_r04k_fill_nt.log)
-  if (A.fill && (&v == &kSegDg8 || &v == &kSegDg8c16 || &v == &kSegDg8c40 || &v == &kSegDg8c32 ||
-                 &v == &kSegDg8c24))
+  if (A.fill && (&v == &kSegDg8 || &v == &kSegDg8c16 || &v == &kSegDg8c40))
     k = v.fn[fill_nt()];
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hip_status(hipGetLastError());
@@ -2603,7 +2592,7 @@ int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
 const Variant &pick_ragged_fill(int mode, uint64_t n, bool fill) {
   const Variant &v = pick_ragged(mode, n);
   if (fill && &v == &kSegDg8)
-    return dg_fill_ch() == 32 ? kSegDg8c32 : dg_fill_ch() == 24 ? kSegDg8c24 : kSegDg8c40;
+    return kSegDg8c40;
   if (!fill || !fill_wb()) return v;
   if (&v == &kSegTx8) return kSegTxW8c48;
   if (&v == &kSegTx8c16) return kSegTxW8c16;
