@@ -1795,6 +1795,11 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
     // the chunk's tiles cover [0, xe); a point at a tile's end (xe itself,
     // when tile-aligned) takes the running sums after that tile
     const bool last = t * T + T >= cur.xe;  // wave-uniform
+    // The wave's next loads go out at raised priority, ahead of the other waves'
+    // sums on its SIMD, so they are in flight sooner (small ragged RX 26.6 -> 26.3
+    // us, U{64..1500} 129.0 -> 127.1; no gain for k_small, a loss for k_lane:
+    // profiles/r04/kbench_ab_r04p_setprio.log)
+    __builtin_amdgcn_s_setprio(2);
     Chunk nn;  // the chunk after next: its loads go out before this
                   // step's tile loads, so waiting on them never waits on those
     if (last) {
@@ -1803,6 +1808,7 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
     }
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
                           end, cn);
+    __builtin_amdgcn_s_setprio(0);
 
 
     const Pos tb = (Pos)(t * T);
