@@ -155,6 +155,8 @@ class Workload:
         if self.offsets is not None:  # validate once; the timed launches skip the check
             batch.checksum_ragged(self.data[0], self.offsets, self.mode,
                                   initial_arr=self.initial_arr, addrs=self.addrs, out=self.out)
+        if self.fill:
+            self.check_fill()
         # algorithmic bytes per launch: payload + side arrays + uint16 out
         self.bytes = self.payload + self.side + 2 * n * batch.outputs(self.mode)
 
@@ -176,6 +178,42 @@ class Workload:
         else:
             batch.checksum_ragged(d, self.offsets, self.mode, initial_arr=self.initial_arr,
                                   out=self.out, validate=False)
+
+    def stored_fields(self, d: torch.Tensor) -> torch.Tensor:
+        """The checksum fields the in-place writer stored into batch d (big-endian), as
+        uint16 values in result order: the transport field per packet (uniform configs
+        9 / 10 and ragged UDP config 13), or [IPv4 field, transport field] per datagram
+        (TX_DATAGRAM config 12, IHL read from each header)."""
+        if self.offsets is None:
+            f = 16 if self.mode == batch.TCP else 6
+            fb = d.view(self.n, self.L)[:, f:f + 2].to(torch.int32)
+            return (fb[:, 0] << 8) | fb[:, 1]
+        s0 = self.offsets[:-1]
+        be16 = lambda at: (d[at].to(torch.int32) << 8) | d[at + 1].to(torch.int32)  # noqa: E731
+        if self.mode == batch.TX_DATAGRAM:
+            hl = (d[s0].to(torch.int64) & 0xF) * 4
+            return torch.stack([be16(s0 + 10), be16(s0 + hl + 16)], dim=1).reshape(-1)
+        return be16(s0 + 6)
+
+    def check_fill(self) -> None:
+        """The timed in-place launches are the writer's kernel (k_seg's TXW / DG forms,
+        k_small / k_lane fill), not the read-only one the result-array calls run: run it
+        once on a copy of batch 0 and require that the fields it stored, and the results
+        it returned, equal the read-only kernel's values (self.out, from the same bytes)."""
+        d = self.data[0].clone()
+        got = torch.empty_like(self.out)
+        if self.offsets is None:
+            batch.checksum_uniform(d, self.L, self.L, self.n, self.mode, initial_arr=self.initial_arr,
+                                   addrs=self.addrs, out=self.out)
+            batch.checksum_uniform(d, self.L, self.L, self.n, self.mode, initial_arr=self.initial_arr,
+                                   addrs=self.addrs, out=got, fill=True)
+        else:
+            batch.checksum_ragged(d, self.offsets, self.mode, initial_arr=self.initial_arr, addrs=self.addrs,
+                                  out=got, fill=True, validate=False)
+        want = self.out.to(torch.int32)
+        if not (torch.equal(got.to(torch.int32), want) and torch.equal(self.stored_fields(d), want)):
+            raise SystemExit(f"config {self.cfg}: the in-place writer disagrees with the read-only kernel")
+        del d
 
     def kernel_name(self) -> str:
         if self.offsets is not None:
@@ -253,15 +291,13 @@ def cpu_baseline(w: Workload, threads: int, budget_s: float):
     w.step(0)
     torch.cuda.synchronize()
     if w.fill:  # the fields written in place (big-endian), against the oracle's values
-        f = 16 if w.mode == batch.TCP else 6
-        fb = w.data[0].view(w.n, w.L)[:, f:f + 2].cpu().numpy()
-        got = (fb[:, 0].astype(np.uint16) << 8) | fb[:, 1]
+        got = w.stored_fields(w.data[0]).cpu().numpy().astype(np.uint16)
     else:
         got = w.out.cpu().numpy()
     if offs is None:
         want = C.batch(host, w.mode, stride=w.L, length=w.L, n=w.n, initial_arr=ia, addrs=ad, threads=threads)
     else:
-        want = C.batch(host, w.mode, offsets=offs, initial_arr=ia, threads=threads)
+        want = C.batch(host, w.mode, offsets=offs, initial_arr=ia, addrs=ad, threads=threads)
     parity = bool(np.array_equal(got, want))
 
     def rate(nthreads, sample_pk):
@@ -272,7 +308,8 @@ def cpu_baseline(w: Workload, threads: int, budget_s: float):
             b = sample_pk * w.L
         else:
             o = offs[:sample_pk + 1]
-            run = lambda: C.batch(host, w.mode, offsets=o, initial_arr=ia, threads=nthreads)  # noqa: E731
+            run = lambda: C.batch(host, w.mode, offsets=o, initial_arr=ia, addrs=ad,  # noqa: E731
+                                  threads=nthreads)
             b = int(o[-1] - o[0])
         b_alg = b + (w.side + 2 * w.n * batch.outputs(w.mode)) * sample_pk / w.n
         reps, t = 0, 0.0
@@ -528,10 +565,13 @@ def _device_count(env=None, nodes: str = KFD_NODES, dri: str = DRI_DIR) -> int:
     launcher starts its ranks before anything here has touched a GPU: the KFD topology
     nodes that are GPUs (gfx_target_version != 0) and whose render node this process
     can open — the enumeration the ROCm runtime does — then cut by
-    ROCR_VISIBLE_DEVICES, HIP_VISIBLE_DEVICES and CUDA_VISIBLE_DEVICES in that order.
+    ROCR_VISIBLE_DEVICES (the ROCr layer), then by ONE HIP-level list:
+    HIP_VISIBLE_DEVICES when it is set and non-empty, else CUDA_VISIBLE_DEVICES when
+    that is (HIP reads the CUDA name only as a fallback; an empty value is no list).
     Opening a render node is a plain DRM file open (no KFD queue, no HIP).
     tests/test_bench_launch.py checks the parsing on a fake topology;
-    tests/test_gpu_dist.py checks the count against torch.cuda.device_count()."""
+    tests/test_gpu_dist.py checks the count against torch.cuda.device_count() for
+    each of these environments, both-set and empty-string ones included."""
     env = os.environ if env is None else env
     n = 0
     try:
@@ -558,9 +598,9 @@ def _device_count(env=None, nodes: str = KFD_NODES, dri: str = DRI_DIR) -> int:
             continue  # not ours (not passed into this container, or no permission)
         os.close(fd)
         n += 1
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        n = _visible_cut(n, env.get(var))
-    return n
+    n = _visible_cut(n, env.get("ROCR_VISIBLE_DEVICES"))
+    hip_list = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES") or None
+    return _visible_cut(n, hip_list)
 
 
 def resolve_launch(gpus: int, env: dict, ndev: int) -> dict:

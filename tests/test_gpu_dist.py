@@ -137,6 +137,26 @@ def test_bench_self_launch_two_ranks_on_one_card(dev):
     assert line["config"]["kernel"] == "k_small<16,6>"
 
 
+@pytest.mark.parametrize("config", [9, 10, 12, 13])
+def test_bench_fill_configs_check_against_oracle(dev, config):
+    """The in-place configs' own line with the CPU baseline on: the workload first
+    checks the writer kernel against the read-only one (Workload.check_fill), then the
+    cpu_baseline leg reads each stored field back (ragged: at offsets[i] + field, both
+    fields of a TX_DATAGRAM) and compares the whole timed batch with the oracle, the
+    side records (config 13's addresses) included."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "YU_BENCH_BACKEND")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", str(config), "--steps", "5",
+                        "--warmup", "2", "--no-extra", "--no-e2e", "--cpu-budget", "1"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["parity_full_batch_vs_oracle"] is True, line
+    assert line["cpu_baseline"]["value"] > 0
+
+
 def _bench_line(n, timeout):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
@@ -181,14 +201,31 @@ def test_host_multi_child_on_one_card(dev):
 
 def test_launcher_device_count_matches_hip(dev):
     """bench._device_count (KFD topology + render nodes, no HIP) against
-    torch.cuda.device_count() in a fresh process, with and without a visibility list."""
+    torch.cuda.device_count() in a fresh process, with and without visibility lists:
+    HIP and CUDA lists set together (HIP's wins), empty strings (no list at the HIP
+    level), an index past the card count, and the ROCr-level list. Every case is
+    run and printed before any assertion, so one run records the runtime's whole
+    behaviour."""
     import bench
     code = "import torch; print(torch.cuda.device_count())"
-    for extra in ({}, {"HIP_VISIBLE_DEVICES": "0"}):
-        env = dict(os.environ, **extra)
+    vis = ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+    base = {k: v for k, v in os.environ.items() if k not in vis}
+    cases = ({}, {"HIP_VISIBLE_DEVICES": "0"}, {"HIP_VISIBLE_DEVICES": ""},
+             {"CUDA_VISIBLE_DEVICES": ""}, {"CUDA_VISIBLE_DEVICES": "0"},
+             {"HIP_VISIBLE_DEVICES": "0", "CUDA_VISIBLE_DEVICES": "7"},
+             {"HIP_VISIBLE_DEVICES": "7", "CUDA_VISIBLE_DEVICES": "0"},
+             {"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": "0"},
+             {"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": "7"},
+             {"ROCR_VISIBLE_DEVICES": "0"}, {"ROCR_VISIBLE_DEVICES": ""})
+    rows = []
+    for extra in cases:
+        env = dict(base, **extra)
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr
-        assert bench._device_count(env) == int(r.stdout.strip().splitlines()[-1]), extra
+        rows.append((extra, bench._device_count(env), int(r.stdout.strip().splitlines()[-1])))
+    for extra, mine, hip in rows:
+        print(f"device count {extra}: launcher {mine}, HIP {hip}")
+    assert all(mine == hip for _, mine, hip in rows), rows
 
 
 def _rccl_rank(port, q):
