@@ -47,7 +47,10 @@ func BatchHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, 
 // in place, like SetChecksum (header/udp.go:60-62, header/tcp.go:156-158,
 // header/ipv4.go:165-167, header/icmpv4.go:46-48). mode is ModeUDP, ModeTCP,
 // ModeIPv4, ModeICMP or ModeTxDatagram (both fields of whole datagrams); out
-// (n results, 2n for ModeTxDatagram) may be nil.
+// (n results, 2n for ModeTxDatagram) may be nil. Like SetChecksum it has no
+// alignment precondition: the CPU stores each field wherever it lies. The
+// errors it returns are include/yucsum.h's Preconditions ([fill-mode] for
+// another mode; [len-transport] for a packet over 65535 bytes; [iov-view]).
 func FillHostPackets(pkts [][]byte, mode Mode, initial []uint16, addrs []byte, out []uint16,
 	device int) error {
 	if len(pkts) == 0 {

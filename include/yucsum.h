@@ -60,6 +60,69 @@ extern "C" {
 #define YU_EHIP_BASE (-1000)    /* -(1000 + hipError_t) for any other HIP error */
 
 /* ------------------------------------------------------------------ */
+/* Preconditions: every YU_EINVAL the batched calls return.            */
+/* Each `return YU_EINVAL` in the library is tagged with one of these   */
+/* names, and tests/test_abi.py checks that the tags and this list      */
+/* agree. All are checked before any device work; a call that returns  */
+/* YU_EINVAL has read no packet byte and written nothing.               */
+/*                                                                      */
+/*  [mode]          mode is not 0 .. YU_MODE_COUNT-1 (every call).       */
+/*  [out]           out == NULL in a yu_csum_batch_* call, or h_out ==   */
+/*                  NULL in a yu_csum_batch_host_* call (the fill calls  */
+/*                  take NULL: no result array).                         */
+/*  [fill-mode]     a fill call (yu_csum_fill_*) with a mode that has no */
+/*                  field to write: RAW, VERIFY_* (or no mode at all).   */
+/*  [side-align]    device calls: initial_arr not 2-byte aligned, addrs  */
+/*                  not 4-byte aligned, out not 2-byte aligned.          */
+/*  [data]          data == NULL with n > 0 (device calls), h_data ==    */
+/*                  NULL while the packets hold bytes (host calls), iov  */
+/*                  == NULL while first_iov names views.                 */
+/*  [len-transport] a packet of a mode other than RAW longer than        */
+/*                  YU_MAX_TRANSPORT_LEN (uniform len; every host ragged */
+/*                  or iov packet). Device ragged batches are not read   */
+/*                  back on the host: see "Out of contract" below.       */
+/*  [len-raw]       a RAW packet longer than YU_MAX_RAW_LEN (the same).  */
+/*  [len-min]       uniform len below the mode's fixed header: UDP 8,    */
+/*                  TCP 20, ICMP 4, IPV4 / VERIFY_IPV4 1 (the IHL byte). */
+/*  [span]          uniform: data + (n-1)*stride + len wraps the address */
+/*                  space.                                               */
+/*  [offsets]       offsets == NULL, or (device) not 8-byte aligned, or  */
+/*                  (host) decreasing; first_iov == NULL or decreasing.  */
+/*  [iov-view]      a view with base == NULL and len > 0.                */
+/*  [fill-align]    yu_csum_fill_uniform: data or stride not a multiple  */
+/*                  of 4. The uniform writers store whole dwords of each */
+/*                  packet's window, so no dword may hold bytes of two   */
+/*                  packets.                                             */
+/*  [fill-overlap]  yu_csum_fill_uniform: n > 1 and stride < len.        */
+/*  [devices]       *_multi: devices == NULL, ndev < 1 or ndev > 64.     */
+/*                  (A listed device that does not exist: YU_ENODEV.)    */
+/*                                                                      */
+/* Where the writers differ from the reference: Go's SetChecksum         */
+/* (header/udp.go:60-62, header/tcp.go:156-158, header/ipv4.go:165-167,  */
+/* header/icmpv4.go:46-48) has no alignment precondition, and neither do */
+/* yu_csum_fill_ragged (device) and the yu_csum_fill_host_* calls: a     */
+/* packed, unaligned tun burst (any data address, any offsets) is        */
+/* written in place as it lies. Only the uniform device writer asks for  */
+/* [fill-align]; an unaligned uniform batch goes through                 */
+/* yu_csum_fill_ragged with offsets[i] = i * stride instead (same values,*/
+/* same field stores). In the ragged writer a field at an even address   */
+/* is one 16-bit store and one at an odd address two byte stores; from   */
+/* 65536 packets on (the TXW kind, yu_ragged_fill_variant_n) the         */
+/* 128-byte lines that lie wholly inside one 48-packet chunk's packets   */
+/* and hold a field are stored whole from the bytes just read, the field */
+/* patched in; a field straddling two lines keeps its byte stores.       */
+/* Bytes outside the packets' fields are never changed.                  */
+/*                                                                      */
+/* Out of contract (device ragged batches only, whose offsets live in    */
+/* device memory and are not checked here): a packet longer than the     */
+/* mode's limit gets an unspecified value, never a fault or a hang. In a */
+/* fill call with such a packet, the field stores of the packet chunk   */
+/* holding it may land elsewhere in [floor4(data + offsets[0]),          */
+/* data + offsets[n]) instead of in the fields. Validate first when the  */
+/* offsets come from outside (the host forms and the Python front end    */
+/* batch.checksum_ragged(validate=True) do).                             */
+
+/* ------------------------------------------------------------------ */
 /* Scalar entry points (host CPU, Go-signature drop-ins).             */
 /* ------------------------------------------------------------------ */
 
@@ -220,7 +283,9 @@ int yu_csum_batch_ragged(const uint8_t *data, const uint64_t *offsets,
  * header/udp.go:60-62, TCP.SetChecksum header/tcp.go:156-158,
  * IPv4.SetChecksum header/ipv4.go:165-167, ICMPv4.SetChecksum
  * header/icmpv4.go:46-48; both fields of a datagram in TX_DATAGRAM).
- * `out` may be NULL. `data` is written. */
+ * `out` may be NULL. `data` is written: the fields only (see Preconditions
+ * above: [fill-mode]; the uniform form also [fill-align], [fill-overlap];
+ * the ragged form takes any alignment). */
 int yu_csum_fill_uniform(uint8_t *data, uint64_t stride, uint32_t len,
                          uint64_t n, int mode,
                          const uint16_t *initial_arr, uint16_t initial,

@@ -239,6 +239,12 @@ inline void Ragged(const uint8_t *data, const uint64_t *offsets, uint64_t n, Mod
   if (rc) throw Error(rc, "yu_csum_batch_ragged");
 }
 
+// In-place writers (SetChecksum on the device; include/yucsum.h, Preconditions).
+// FillUniform needs data and stride multiples of 4 and stride >= len (else Error with
+// YU_EINVAL: [fill-align], [fill-overlap]); FillRagged takes any alignment — a packed,
+// unaligned tun burst as it lies — so an unaligned uniform batch goes through
+// FillRagged with offsets[i] = i * stride. Only the fields change. Both throw
+// YU_EINVAL for a mode with no field ([fill-mode]: RAW, VERIFY_*).
 inline void FillUniform(uint8_t *data, uint64_t stride, uint32_t len, uint64_t n, Mode m,
                         uint16_t *out = nullptr, const Side &s = {}, void *stream = nullptr) {
   int rc = yu_csum_fill_uniform(data, stride, len, n, m, s.initial_arr, s.initial, s.addrs,
@@ -302,7 +308,8 @@ inline void HostPackets(const yu_iovec *iov, const uint64_t *first_iov, uint64_t
 }
 
 // Host-memory field writer (SetChecksum in place, TX modes): the batch above,
-// then each result stored big-endian into the packet's field. `out` may be null.
+// then each result stored big-endian into the packet's field by the CPU, at any
+// alignment (as Go's SetChecksum). `out` may be null.
 inline void FillHostUniform(uint8_t *data, uint64_t stride, uint32_t len, uint64_t n, Mode m,
                             uint16_t *out = nullptr, const Side &s = {}, int device = 0) {
   int rc = yu_csum_fill_host_uniform(data, stride, len, n, m, s.initial_arr, s.initial, s.addrs,

@@ -213,3 +213,141 @@ def test_sparse_datagram_batches_leave_k_seg(mode, kern, loop):
     assert batch.variant(1500, 1500, mode, 0, n=n) == kern
     assert batch.variant(SEG32_STRIDE, 1500, mode, 0, n=n) == kern
     assert batch.variant(SEG32_STRIDE + 1, 1500, mode, 0, n=n) == loop
+
+
+_KNOB_PROBE = (
+    "import sys; sys.path.insert(0, %r)\n"
+    "from yustack_amd import _lib\n"
+    "L = _lib.lib()\n"
+    "print(L.yu_ragged_variant_n(0, 1 << 20).decode(), L.yu_uniform_variant_n(1500, 1500, 1 << 20, 2, 0).decode(),\n"
+    "      L.yu_ragged_fill_variant_n(1, 1 << 20).decode())\n" % ROOT)
+
+
+def _variants_under(env_extra):
+    env = {k: v for k, v in os.environ.items() if not k.startswith("YU_")}
+    env.update(env_extra)
+    r = subprocess.run([__import__("sys").executable, "-c", _KNOB_PROBE], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.split(), r.stderr
+
+
+def test_tuning_knobs_need_the_gate():
+    """The measurement knobs (YU_RAGGED, YU_VARIANT, YU_FILL_WB, ...) change the
+    kernel choice only when YU_TUNING=1 is set too; an inherited knob alone leaves
+    the library's own choice (the reference's whole config surface
+    is two package variables, link/tundev/tundev.go:20 and link/sniffer/sniffer.go:14)."""
+    knobs = {"YU_RAGGED": "loop", "YU_VARIANT": "k_small<32,4>", "YU_FILL_WB": "0", "YU_NT": "1"}
+    default, err0 = _variants_under({})
+    assert default == ["k_seg<8>", "k_small<16,6>", "k_seg<8,txw,c48>"]
+    inherited, err1 = _variants_under(knobs)
+    assert inherited == default and "tuning knob" not in err1
+    for bad_gate in ("0", "yes", "11", ""):
+        assert _variants_under(dict(knobs, YU_TUNING=bad_gate))[0] == default
+    tuned, err2 = _variants_under(dict(knobs, YU_TUNING="1"))
+    assert tuned == ["k_loop<4,BE>", "k_small<32,4>", "k_loop<4,LE>"]
+    # the open gate names each knob it reads
+    assert "tuning knob YU_RAGGED=loop" in err2 and "tuning knob YU_VARIANT=k_small<32,4>" in err2
+    # YU_FILL_WB alone (no forced ragged kernel): the TX kind instead of TXW
+    assert _variants_under({"YU_TUNING": "1", "YU_FILL_WB": "0"})[0][2] == "k_seg<8,tx>"
+
+
+SOURCES = [os.path.join(ROOT, "yustack_amd", "csrc", f) for f in ("yucsum_kernels.hip", "yucsum_host.cpp",
+                                                                  "yucsum_scalar.cpp")]
+
+
+def _header_einval_tags():
+    src = open(HEADER).read()
+    block = src[src.index("Preconditions: every YU_EINVAL"):src.index("Where the writers differ")]
+    return set(re.findall(r"/\*\s+\[([a-z-]+)\]", block))
+
+
+def test_every_einval_is_documented():
+    """Static check: each `return YU_EINVAL` in the library
+    carries an `EINVAL:<tag>` comment, every tag is one include/yucsum.h's
+    Preconditions list documents, and every documented tag is used."""
+    documented = _header_einval_tags()
+    assert len(documented) >= 14, documented
+    used = set()
+    for path in SOURCES:
+        lines = open(path).read().splitlines()
+        for k, line in enumerate(lines):
+            if "return YU_EINVAL" not in line:
+                continue
+            m = re.search(r"EINVAL:([a-z-]+(?: / [a-z-]+)*)", line)
+            assert m, f"{os.path.basename(path)}:{k + 1}: untagged YU_EINVAL: {line.strip()}"
+            for tag in m.group(1).split(" / "):
+                assert tag in documented, f"{os.path.basename(path)}:{k + 1}: [{tag}] not in yucsum.h"
+                used.add(tag)
+    assert used == documented, documented ^ used
+
+
+def test_each_documented_einval_is_returned():
+    """One call per documented precondition, each returning YU_EINVAL before any
+    device work (so on this GPU-less host too); plus the cases the header states
+    are NOT errors (an unaligned ragged fill, NULL out in a fill call), which get
+    past validation and stop at the missing device."""
+    L = _lib.lib()
+    EINVAL = _lib.YU_EINVAL
+    buf = (ctypes.c_uint8 * 256)()
+    out = (ctypes.c_uint16 * 8)()
+    p, o = ctypes.addressof(buf), ctypes.addressof(out)
+    offs = (ctypes.c_uint64 * 5)(0, 16, 32, 48, 64)
+    po = ctypes.addressof(offs)
+    dec = (ctypes.c_uint64 * 5)(0, 16, 8, 48, 64)
+    iov = (_lib.YuIovec * 4)(*[_lib.YuIovec(p + 16 * i, 16) for i in range(4)])
+    first = (ctypes.c_uint64 * 5)(0, 1, 2, 3, 4)
+    devs = (ctypes.c_int * 2)(0, 0)
+    pd = ctypes.addressof(devs)
+    cases = {
+        "mode": [L.yu_csum_batch_uniform(p, 16, 16, 4, YU_MODE_COUNT, None, 0, None, o, None),
+                 L.yu_csum_batch_ragged(p, po, 4, -1, None, 0, None, o, None),
+                 L.yu_csum_batch_host_ragged(p, po, 4, 10, None, 0, None, o, 0),
+                 L.yu_csum_batch_host_iov_multi(ctypes.addressof(iov), ctypes.addressof(first), 4, 99, None, 0,
+                                                None, o, pd, 2)],
+        "out": [L.yu_csum_batch_ragged(p, po, 4, 0, None, 0, None, None, None),
+                L.yu_csum_batch_host_uniform(p, 16, 16, 4, 0, None, 0, None, None, 0)],
+        "fill-mode": [L.yu_csum_fill_uniform(p, 16, 16, 4, 0, None, 0, None, o, None),  # RAW
+                      L.yu_csum_fill_ragged(p, po, 4, 8, None, 0, None, o, None),        # VERIFY_RX
+                      L.yu_csum_fill_host_ragged(p, po, 4, 5, None, 0, None, o, 0)],     # VERIFY_IPV4
+        "side-align": [L.yu_csum_batch_uniform(p, 16, 16, 4, 0, p + 1, 0, None, o, None),
+                       L.yu_csum_batch_uniform(p, 16, 16, 4, 1, None, 0, p + 2, o, None),
+                       L.yu_csum_batch_ragged(p, po, 4, 0, None, 0, None, o + 1, None)],
+        "data": [L.yu_csum_batch_uniform(None, 16, 16, 4, 0, None, 0, None, o, None),
+                 L.yu_csum_batch_ragged(None, po, 4, 0, None, 0, None, o, None),
+                 L.yu_csum_batch_host_uniform(None, 16, 16, 4, 0, None, 0, None, o, 0),
+                 L.yu_csum_batch_host_ragged(None, po, 4, 0, None, 0, None, o, 0)],
+        "len-transport": [L.yu_csum_batch_uniform(p, 16, 65536, 1, 2, None, 0, None, o, None),
+                          L.yu_csum_batch_host_uniform(p, 16, 65536, 1, 1, None, 0, None, o, 0)],
+        "len-raw": [L.yu_csum_batch_uniform(p, 16, 0xFFFF0001, 1, 0, None, 0, None, o, None)],
+        "len-min": [L.yu_csum_batch_uniform(p, 16, 7, 4, 1, None, 0, None, o, None),    # UDP < 8
+                    L.yu_csum_batch_uniform(p, 32, 19, 4, 2, None, 0, None, o, None),   # TCP < 20
+                    L.yu_csum_batch_uniform(p, 16, 3, 4, 4, None, 0, None, o, None),    # ICMP < 4
+                    L.yu_csum_batch_uniform(p, 16, 0, 4, 3, None, 0, None, o, None)],   # IPv4: no IHL byte
+        "span": [L.yu_csum_batch_uniform(p, 1 << 62, 16, 5, 0, None, 0, None, o, None)],
+        "offsets": [L.yu_csum_batch_ragged(p, None, 4, 0, None, 0, None, o, None),
+                    L.yu_csum_batch_ragged(p, po + 4, 4, 0, None, 0, None, o, None),
+                    L.yu_csum_batch_host_ragged(p, ctypes.addressof(dec), 4, 0, None, 0, None, o, 0),
+                    L.yu_csum_batch_host_iov(ctypes.addressof(iov), None, 4, 0, None, 0, None, o, 0)],
+        "iov-view": [L.yu_csum_batch_host_iov(None, ctypes.addressof(first), 4, 0, None, 0, None, o, 0)],
+        "fill-align": [L.yu_csum_fill_uniform(p + 2, 16, 16, 4, 1, None, 0, None, o, None),
+                       L.yu_csum_fill_uniform(p, 18, 16, 4, 1, None, 0, None, o, None)],
+        "fill-overlap": [L.yu_csum_fill_uniform(p, 16, 20, 4, 1, None, 0, None, o, None)],
+        "devices": [L.yu_csum_batch_host_uniform_multi(p, 16, 16, 4, 0, None, 0, None, o, None, 2),
+                    L.yu_csum_batch_host_ragged_multi(p, po, 4, 0, None, 0, None, o, pd, 0),
+                    L.yu_csum_batch_host_iov_multi(ctypes.addressof(iov), ctypes.addressof(first), 4, 0, None,
+                                                   0, None, o, pd, 65)],
+    }
+    assert set(cases) == _header_einval_tags()
+    for tag, rcs in cases.items():
+        assert all(rc == EINVAL for rc in rcs), (tag, rcs)
+    if not torch.cuda.is_available():
+        # documented as accepted: they pass validation and stop at the missing device
+        nodev = _lib.YU_ENODEV
+        uo = (ctypes.c_uint64 * 5)(1, 18, 33, 51, 64)  # odd offsets
+        assert L.yu_csum_fill_ragged(p + 1, ctypes.addressof(uo), 4, 1, None, 0, None, None, None) == nodev
+        assert L.yu_csum_fill_ragged(p + 3, po, 4, 9, None, 0, None, o, None) == nodev
+        assert L.yu_csum_fill_host_ragged(p + 1, ctypes.addressof(uo), 4, 1, None, 0, None, None, 0) == nodev
+
+
+YU_MODE_COUNT = 10

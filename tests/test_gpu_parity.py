@@ -13,9 +13,11 @@ import torch
 from oracle import oracle as O
 from yustack_amd import batch
 
-# a measurement run that forces the ragged kernel (YU_RAGGED) checks parity only:
-# the default ragged kernel choice is not asserted then
-FORCED = bool(os.environ.get("YU_RAGGED"))
+# a measurement run that forces the ragged kernel (YU_TUNING=1 YU_RAGGED=...) checks
+# parity only: the default ragged kernel choice is not asserted then. The library
+# reads its knobs only under the YU_TUNING=1 gate, and so do these flags.
+TUNING = os.environ.get("YU_TUNING") == "1"
+FORCED = TUNING and bool(os.environ.get("YU_RAGGED"))
 # TX_DATAGRAM in place from 64K datagrams on: 40-packet chunks
 DG_FILL_CH = 40
 DG_FILL = f"k_seg<8,dg,c{DG_FILL_CH}>"
@@ -351,18 +353,25 @@ def test_tx_datagram_ragged(dev, oracle_c, npk):
     assert (rx[l4_def] & (O.RX_L4 | O.RX_L4_OK) == (O.RX_L4 | O.RX_L4_OK)).all()
 
 
-@pytest.mark.parametrize("shift", [0, 68])
+@pytest.mark.parametrize("packed,shift", [(False, 0), (False, 68), (True, 0), (True, 1), (True, 67),
+                                          (True, 130)])
 @pytest.mark.parametrize("npk", [5000, 70000])
 @pytest.mark.parametrize("mode,lo", [(O.MODE_UDP, 8), (O.MODE_TCP, 20), (O.MODE_ICMP, 4)])
-def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, shift):
-    """In place on ragged small packets (4-aligned offsets, the fill contract) with a
-    few large ones among them, in 16- and 64-packet k_seg chunks: only the fields
-    change, chunk edges included, and the results equal the oracle's. The TX kind's
-    whole-line write-back (YU_FILL_WB) stores the 128-byte lines of each chunk's last
-    tile; shift 68 starts the batch off a line boundary, so the first chunk's line
-    begins before the batch."""
-    rng = np.random.default_rng(9900 + 7 * mode + npk)
-    lens = (rng.integers(lo, 201, size=npk) + 3) & ~3
+def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, packed, shift):
+    """In place on ragged small packets with a few large ones among them, in 16- and
+    48-packet k_seg chunks: only the fields change, chunk edges included, and the
+    results equal the oracle's. The TX kind's whole-line write-back (YU_FILL_WB)
+    stores the 128-byte lines of each chunk's last tile; shift 68 starts the batch
+    off a line boundary, so the first chunk's line begins before the batch.
+    `packed`: lengths as drawn (not rounded to 4) and the batch at an odd address
+    (shift 1, 67) or 2 bytes past a line (130) — a packed, unaligned tun burst, which
+    yu_csum_fill_ragged takes as it lies (include/yucsum.h, Preconditions): fields at
+    odd addresses and fields straddling a 128-byte line, in the TXW kind's 48-packet
+    chunks from 70000 packets."""
+    rng = np.random.default_rng(9900 + 7 * mode + npk + (1000 if packed else 0))
+    lens = rng.integers(lo, 201, size=npk)
+    if not packed:
+        lens = (lens + 3) & ~3
     lens[rng.choice(npk, size=npk // 500, replace=False)] = 4 * rng.integers(1000, 2500, size=npk // 500)
     offs = np.zeros(npk + 1, np.uint64)
     offs[1:] = np.cumsum(lens)
@@ -373,7 +382,7 @@ def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, shift):
     want = oracle_c.batch(blob, mode, offsets=offs, addrs=addrs if mode != O.MODE_ICMP else None)
     # the write-back off (YU_FILL_WB=0): the TX kind; from 64K packets on the TXW kind
     # takes 48-packet chunks
-    wb = os.environ.get("YU_FILL_WB") != "0"
+    wb = not (TUNING and os.environ.get("YU_FILL_WB") == "0")
     big = "k_seg<8,txw,c48>" if wb else "k_seg<8,tx>"
     assert FORCED or batch.ragged_variant(mode, npk, fill=True) == (
         f"k_seg<8,{'txw' if wb else 'tx'},c16>" if npk < 65536 else big)
@@ -391,13 +400,15 @@ def test_fill_ragged_small_packets(dev, oracle_c, mode, lo, npk, shift):
     bad = np.nonzero(d.cpu().numpy() != exp)[0]
     assert bad.size == 0, bad[:10]
     assert np.array_equal(whole[:shift].cpu().numpy(), pre)  # the bytes before the batch
+    if packed:  # the layout did put fields on odd addresses and across 128-byte lines
+        fa = fi + shift
+        assert (fa & 1).any() and ((fa & 127) == 127).any()
 
 
 def test_tx_datagram_fuzz(dev, oracle_c):
     """Seeded TX_DATAGRAM batches of 1 to 70000 datagrams: random sizes (tiny, MTU,
     jumbo), protocols, IHL 5..15, a share damaged or out of contract, random start
-    alignment (values) and 4-aligned placement (in place, where only the defined
-    fields may change). YU_TX_FUZZ_SEED / YU_TX_FUZZ_ITERS for longer runs by hand."""
+    alignment (values, and in place, where only the defined fields may change). YU_TX_FUZZ_SEED / YU_TX_FUZZ_ITERS for longer runs by hand."""
     import os
     import rxgen
     rng = np.random.default_rng(int(os.environ.get("YU_TX_FUZZ_SEED", "5151")))
@@ -417,7 +428,7 @@ def test_tx_datagram_fuzz(dev, oracle_c):
         got = batch.checksum_ragged(_to(dev, b), _to(dev, (offs + base_off).view(np.int64)),
                                     "tx_datagram").cpu().numpy()
         assert np.array_equal(got, want), (it, npk, lo, hi, base_off, np.nonzero(got != want)[0][:10])
-        pad = 4 * int(rng.integers(0, 4))
+        pad = int(rng.integers(0, 16))  # in place at any alignment (include/yucsum.h)
         d = _to(dev, np.concatenate([np.zeros(pad, np.uint8), blob, np.zeros(32, np.uint8)]))
         got = batch.checksum_ragged(d, _to(dev, (offs + pad).view(np.int64)), "tx_datagram",
                                     fill=True).cpu().numpy()
@@ -1330,7 +1341,8 @@ def test_random_batches_fuzz(dev, oracle_c):
             blob = _rand(rng, int(offs[-1]) + 16, ["rand", "rand", "rand", "zero", "ff"][it % 5])
             _fuzz_headers(rng, blob, offs[:-1], lens, mode)
             want = oracle_c.batch(blob, mode, offsets=offs, initial_arr=init, initial=initial, addrs=addrs)
-            d = _to(dev, blob)
+            dshift = it % 4  # the data pointer itself at every alignment (no rng draw)
+            d = _to(dev, np.concatenate([np.zeros(dshift, np.uint8), blob]))[dshift:]
             seen.add(batch.ragged_variant(mode, n, fill=fill))
             got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), mode, initial=initial,
                                         initial_arr=None if init is None else _to(dev, init),

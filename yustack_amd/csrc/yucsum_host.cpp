@@ -171,7 +171,7 @@ class CopyPool {
 
  private:
   CopyPool() {
-    const char *e = getenv("YU_HOST_COPY_THREADS");
+    const char *e = yu::tuning_env("YU_HOST_COPY_THREADS");
     nthreads_ = e && *e ? atoi(e) : 7;
     if (nthreads_ < 0) nthreads_ = 0;
     if (nthreads_ > 64) nthreads_ = 64;
@@ -274,7 +274,7 @@ constexpr int kNoDirect = 1;  // not an error: take the pipelined path
 
 uint64_t direct_max() {
   static const uint64_t v = [] {
-    const char *e = getenv("YU_HOST_DIRECT_MAX");
+    const char *e = yu::tuning_env("YU_HOST_DIRECT_MAX");
     return e && *e ? strtoull(e, nullptr, 10) : (uint64_t)(4ull << 20);
   }();
   return v;
@@ -573,8 +573,10 @@ bool span_wraps(const uint8_t *data, uint64_t stride, uint32_t len, uint64_t n) 
 // every packet within the mode's length limit.
 int check_offsets(const uint64_t *off, uint64_t n, int mode) {
   const uint64_t cap = mode == YU_MODE_RAW ? YU_MAX_RAW_LEN : YU_MAX_TRANSPORT_LEN;
-  for (uint64_t i = 0; i < n; ++i)
-    if (off[i + 1] < off[i] || off[i + 1] - off[i] > cap) return YU_EINVAL;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (off[i + 1] < off[i]) return YU_EINVAL;        // EINVAL:offsets
+    if (off[i + 1] - off[i] > cap) return YU_EINVAL;  // EINVAL:len-transport / len-raw
+  }
   return YU_OK;
 }
 
@@ -583,11 +585,12 @@ int check_offsets(const uint64_t *off, uint64_t n, int mode) {
 int check_iov(const yu_iovec *iov, const uint64_t *first_iov, uint64_t n, int mode) {
   const uint64_t cap = mode == YU_MODE_RAW ? YU_MAX_RAW_LEN : YU_MAX_TRANSPORT_LEN;
   for (uint64_t i = 0; i < n; ++i) {
-    if (first_iov[i + 1] < first_iov[i]) return YU_EINVAL;
+    if (first_iov[i + 1] < first_iov[i]) return YU_EINVAL;  // EINVAL:offsets
     uint64_t l = 0;
     for (uint64_t v = first_iov[i]; v < first_iov[i + 1]; ++v) {
-      if (!iov[v].base && iov[v].len) return YU_EINVAL;
-      if (iov[v].len > cap - l) return YU_EINVAL;  // l <= cap: no wrap, even for huge views
+      if (!iov[v].base && iov[v].len) return YU_EINVAL;  // EINVAL:iov-view
+      // l <= cap: no wrap, even for huge views
+      if (iov[v].len > cap - l) return YU_EINVAL;  // EINVAL:len-transport / len-raw
       l += iov[v].len;
     }
   }
@@ -706,12 +709,13 @@ extern "C" int yu_csum_batch_host_uniform(const uint8_t *h_data,
                                           uint16_t initial,
                                           const uint8_t *h_addrs,
                                           uint16_t *h_out, int device) {
-  if (bad_mode(mode) || !h_out) return YU_EINVAL;
+  if (bad_mode(mode)) return YU_EINVAL;  // EINVAL:mode
+  if (!h_out) return YU_EINVAL;          // EINVAL:out
   if (n == 0) return YU_OK;
-  if (!h_data && len) return YU_EINVAL;
-  if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
-  if (len > YU_MAX_RAW_LEN) return YU_EINVAL;
-  if (span_wraps(h_data, stride, len, n)) return YU_EINVAL;
+  if (!h_data && len) return YU_EINVAL;                                      // EINVAL:data
+  if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;  // EINVAL:len-transport
+  if (len > YU_MAX_RAW_LEN) return YU_EINVAL;                                // EINVAL:len-raw
+  if (span_wraps(h_data, stride, len, n)) return YU_EINVAL;                  // EINVAL:span
   return on_device(device, [&](Ctx &c) {
     const uint64_t pstride = stride ? stride : 1;
     uint64_t slice = kSliceBytes / pstride;
@@ -728,9 +732,11 @@ extern "C" int yu_csum_batch_host_ragged(const uint8_t *h_data,
                                          uint16_t initial,
                                          const uint8_t *h_addrs,
                                          uint16_t *h_out, int device) {
-  if (bad_mode(mode) || !h_out) return YU_EINVAL;
+  if (bad_mode(mode)) return YU_EINVAL;  // EINVAL:mode
+  if (!h_out) return YU_EINVAL;          // EINVAL:out
   if (n == 0) return YU_OK;
-  if (!h_offsets || (!h_data && h_offsets[n] != h_offsets[0])) return YU_EINVAL;
+  if (!h_offsets) return YU_EINVAL;                                   // EINVAL:offsets
+  if (!h_data && h_offsets[n] != h_offsets[0]) return YU_EINVAL;     // EINVAL:data
   if (int rc = check_offsets(h_offsets, n, mode)) return rc;
   return on_device(device, [&](Ctx &c) {
     RaggedLayout L{h_data, h_offsets, n, mode, initial, is_pinned(h_data)};
@@ -743,9 +749,11 @@ extern "C" int yu_csum_batch_host_iov(const yu_iovec *iov,
                                       int mode, const uint16_t *h_initial_arr,
                                       uint16_t initial, const uint8_t *h_addrs,
                                       uint16_t *h_out, int device) {
-  if (bad_mode(mode) || !h_out) return YU_EINVAL;
+  if (bad_mode(mode)) return YU_EINVAL;  // EINVAL:mode
+  if (!h_out) return YU_EINVAL;          // EINVAL:out
   if (n == 0) return YU_OK;
-  if (!first_iov || (!iov && first_iov[n] != first_iov[0])) return YU_EINVAL;
+  if (!first_iov) return YU_EINVAL;                                   // EINVAL:offsets
+  if (!iov && first_iov[n] != first_iov[0]) return YU_EINVAL;        // EINVAL:iov-view
   if (int rc = check_iov(iov, first_iov, n, mode)) return rc;
   return on_device(device, [&](Ctx &c) {
     IovLayout L{iov, first_iov, n, mode, initial};
@@ -759,12 +767,14 @@ extern "C" int yu_csum_batch_host_uniform_multi(const uint8_t *h_data, uint64_t 
                                                 uint16_t initial, const uint8_t *h_addrs,
                                                 uint16_t *h_out, const int *devices,
                                                 int ndev) {
-  if (bad_mode(mode) || !h_out || bad_devices(devices, ndev)) return YU_EINVAL;
+  if (bad_mode(mode)) return YU_EINVAL;                // EINVAL:mode
+  if (!h_out) return YU_EINVAL;                        // EINVAL:out
+  if (bad_devices(devices, ndev)) return YU_EINVAL;    // EINVAL:devices
   if (n == 0) return YU_OK;
-  if (!h_data && len) return YU_EINVAL;
-  if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
-  if (len > YU_MAX_RAW_LEN) return YU_EINVAL;
-  if (span_wraps(h_data, stride, len, n)) return YU_EINVAL;
+  if (!h_data && len) return YU_EINVAL;                                      // EINVAL:data
+  if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;  // EINVAL:len-transport
+  if (len > YU_MAX_RAW_LEN) return YU_EINVAL;                                // EINVAL:len-raw
+  if (span_wraps(h_data, stride, len, n)) return YU_EINVAL;                  // EINVAL:span
   if (int rc = check_devices(devices, ndev)) return rc;
   return fan_out(devices, ndev, even_bounds(n, ndev), [&](int i, uint64_t a, uint64_t cnt) {
     return yu_csum_batch_host_uniform(h_data ? h_data + a * stride : nullptr, stride, len, cnt,
@@ -779,9 +789,12 @@ extern "C" int yu_csum_batch_host_ragged_multi(const uint8_t *h_data,
                                                uint16_t initial, const uint8_t *h_addrs,
                                                uint16_t *h_out, const int *devices,
                                                int ndev) {
-  if (bad_mode(mode) || !h_out || bad_devices(devices, ndev)) return YU_EINVAL;
+  if (bad_mode(mode)) return YU_EINVAL;                // EINVAL:mode
+  if (!h_out) return YU_EINVAL;                        // EINVAL:out
+  if (bad_devices(devices, ndev)) return YU_EINVAL;    // EINVAL:devices
   if (n == 0) return YU_OK;
-  if (!h_offsets || (!h_data && h_offsets[n] != h_offsets[0])) return YU_EINVAL;
+  if (!h_offsets) return YU_EINVAL;                                   // EINVAL:offsets
+  if (!h_data && h_offsets[n] != h_offsets[0]) return YU_EINVAL;     // EINVAL:data
   if (int rc = check_offsets(h_offsets, n, mode)) return rc;
   if (int rc = check_devices(devices, ndev)) return rc;
   return fan_out(devices, ndev, byte_bounds(h_offsets, n, ndev),
@@ -798,9 +811,12 @@ extern "C" int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t 
                                             const uint16_t *h_initial_arr, uint16_t initial,
                                             const uint8_t *h_addrs, uint16_t *h_out,
                                             const int *devices, int ndev) {
-  if (bad_mode(mode) || !h_out || bad_devices(devices, ndev)) return YU_EINVAL;
+  if (bad_mode(mode)) return YU_EINVAL;                // EINVAL:mode
+  if (!h_out) return YU_EINVAL;                        // EINVAL:out
+  if (bad_devices(devices, ndev)) return YU_EINVAL;    // EINVAL:devices
   if (n == 0) return YU_OK;
-  if (!first_iov || (!iov && first_iov[n] != first_iov[0])) return YU_EINVAL;
+  if (!first_iov) return YU_EINVAL;                                   // EINVAL:offsets
+  if (!iov && first_iov[n] != first_iov[0]) return YU_EINVAL;        // EINVAL:iov-view
   if (int rc = check_iov(iov, first_iov, n, mode)) return rc;
   if (int rc = check_devices(devices, ndev)) return rc;
   return fan_out(devices, ndev, even_bounds(n, ndev), [&](int i, uint64_t a, uint64_t cnt) {
@@ -902,7 +918,7 @@ extern "C" int yu_csum_fill_host_uniform(uint8_t *h_data, uint64_t stride, uint3
                                          uint64_t n, int mode, const uint16_t *h_initial_arr,
                                          uint16_t initial, const uint8_t *h_addrs,
                                          uint16_t *h_out, int device) {
-  if (!tx_mode(mode)) return YU_EINVAL;
+  if (!tx_mode(mode)) return YU_EINVAL;  // EINVAL:fill-mode (bad mode too)
   if (n == 0) return YU_OK;
   ResultBuf r(h_out, n * YU_MODE_OUTPUTS(mode));
   if (!r.p) return YU_ENOMEM;
@@ -919,7 +935,7 @@ extern "C" int yu_csum_fill_host_ragged(uint8_t *h_data, const uint64_t *h_offse
                                         int mode, const uint16_t *h_initial_arr,
                                         uint16_t initial, const uint8_t *h_addrs,
                                         uint16_t *h_out, int device) {
-  if (!tx_mode(mode)) return YU_EINVAL;
+  if (!tx_mode(mode)) return YU_EINVAL;  // EINVAL:fill-mode (bad mode too)
   if (n == 0) return YU_OK;
   ResultBuf r(h_out, n * YU_MODE_OUTPUTS(mode));
   if (!r.p) return YU_ENOMEM;
@@ -935,7 +951,7 @@ extern "C" int yu_csum_fill_host_ragged(uint8_t *h_data, const uint64_t *h_offse
 extern "C" int yu_csum_fill_host_iov(const yu_iovec *iov, const uint64_t *first_iov, uint64_t n,
                                      int mode, const uint16_t *h_initial_arr, uint16_t initial,
                                      const uint8_t *h_addrs, uint16_t *h_out, int device) {
-  if (!tx_mode(mode)) return YU_EINVAL;
+  if (!tx_mode(mode)) return YU_EINVAL;  // EINVAL:fill-mode (bad mode too)
   if (n == 0) return YU_OK;
   ResultBuf r(h_out, n * YU_MODE_OUTPUTS(mode));
   if (!r.p) return YU_ENOMEM;

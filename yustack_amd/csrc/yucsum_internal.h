@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "yucsum.h"
 
@@ -39,6 +41,24 @@ __host__ __device__ inline uint32_t l4_field(uint32_t proto) {
 }
 __host__ __device__ inline uint32_t l4_min(uint32_t proto) {
   return proto == 17u ? 8u : (proto == 6u ? 20u : (proto == 1u ? 4u : 0u));
+}
+
+// Measurement knobs (YU_RAGGED, YU_VARIANT, YU_NT, YU_FILL_WB, YU_RUNS,
+// YU_BLOCKS_PER_CU, YU_SEG_SMALL_BLOCKS, YU_XCD, YU_HOST_COPY_THREADS,
+// YU_HOST_DIRECT_MAX) force kernels, grids and cut-overs for tools/ and the
+// forced-kernel test runs. They are read only when the process also sets
+// YU_TUNING=1, so a production process that inherits one of them keeps the
+// library's own choices; when the gate is open, each knob that is set is named
+// once on stderr. Returns the knob's value, or NULL (gate closed or unset).
+inline const char *tuning_env(const char *name) {
+  static const bool on = [] {
+    const char *g = getenv("YU_TUNING");
+    return g && g[0] == '1' && g[1] == '\0';
+  }();
+  if (!on) return nullptr;
+  const char *v = getenv(name);
+  if (v && *v) fprintf(stderr, "yucsum: tuning knob %s=%s (YU_TUNING=1)\n", name, v);
+  return v;
 }
 
 }  // namespace yu

@@ -2356,7 +2356,7 @@ constexpr uint64_t kSeg32Stride = ((1ull << 31) - 65535u - 3u) / 63u;
 constexpr uint64_t kMidBatch = 65536;
 
 const Variant &pick_ragged(int mode, uint64_t n) {
-  static const char *f = getenv("YU_RAGGED");
+  static const char *f = yu::tuning_env("YU_RAGGED");
   const bool seg4 = f && strcmp(f, "seg4") == 0;
   const bool rx = mode == YU_MODE_VERIFY_RX;  // only k_seg verifies whole datagrams
   const bool dg = mode == YU_MODE_TX_DATAGRAM;  // and fills both fields of one
@@ -2375,10 +2375,10 @@ const Variant &pick_ragged(int mode, uint64_t n) {
   return seg_for(!seg4, mode);
 }
 
-// Tuning override (measurement only): YU_VARIANT=<name> forces a k_small
-// variant whenever it covers the shape.
+// Tuning override (measurement only, read under YU_TUNING=1: yu::tuning_env):
+// YU_VARIANT=<name> forces a k_small variant whenever it covers the shape.
 const char *forced_variant() {
-  static const char *v = getenv("YU_VARIANT");
+  static const char *v = yu::tuning_env("YU_VARIANT");
   return v;
 }
 
@@ -2467,10 +2467,11 @@ int cu_count(int dev) {
   return c;
 }
 
-// Tuning knobs (read once, measurement only). YU_BLOCKS_PER_CU: grid size in
-// 256-thread blocks per CU; YU_NT: load policy 0/1/2 (see bld16).
+// Tuning knobs (read once, measurement only, and only under YU_TUNING=1:
+// yu::tuning_env). YU_BLOCKS_PER_CU: grid size in 256-thread blocks per CU;
+// YU_NT: load policy 0/1/2 (see bld16).
 int env_int(const char *name, int lo, int hi, int dflt) {
-  const char *s = getenv(name);
+  const char *s = yu::tuning_env(name);
   if (!s || !*s) return dflt;
   int x = atoi(s);
   return (x >= lo && x <= hi) ? x : dflt;
@@ -2583,12 +2584,12 @@ bool aligned(const void *p, uintptr_t a) {
 
 int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
                  const uint16_t *out, bool fill) {
-  if (mode < 0 || mode >= YU_MODE_COUNT) return YU_EINVAL;
-  if (!out && !fill) return YU_EINVAL;
-  if (fill && !mode_fills(mode)) return YU_EINVAL;
-  if (initial_arr && !aligned(initial_arr, 2)) return YU_EINVAL;
-  if (addrs && !aligned(addrs, 4)) return YU_EINVAL;
-  if (out && !aligned(out, 2)) return YU_EINVAL;
+  if (mode < 0 || mode >= YU_MODE_COUNT) return YU_EINVAL;  // EINVAL:mode
+  if (!out && !fill) return YU_EINVAL;                     // EINVAL:out
+  if (fill && !mode_fills(mode)) return YU_EINVAL;         // EINVAL:fill-mode
+  if (initial_arr && !aligned(initial_arr, 2)) return YU_EINVAL;  // EINVAL:side-align
+  if (addrs && !aligned(addrs, 4)) return YU_EINVAL;              // EINVAL:side-align
+  if (out && !aligned(out, 2)) return YU_EINVAL;                  // EINVAL:side-align
   return YU_OK;
 }
 
@@ -2613,15 +2614,17 @@ int batch_uniform(const uint8_t *data, uint8_t *fill, uint64_t stride,
   int rc = check_common(mode, initial_arr, addrs, out, fill != nullptr);
   if (rc) return rc;
   if (n == 0) return YU_OK;
-  if (!data) return YU_EINVAL;
-  if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;
-  if (len < min_len(mode)) return YU_EINVAL;
-  if (len > YU_MAX_RAW_LEN) return YU_EINVAL;  // window offsets stay in uint32
+  if (!data) return YU_EINVAL;                                              // EINVAL:data
+  if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;  // EINVAL:len-transport
+  if (len < min_len(mode)) return YU_EINVAL;                                // EINVAL:len-min
+  if (len > YU_MAX_RAW_LEN) return YU_EINVAL;  // EINVAL:len-raw (window offsets stay in uint32)
   // the batch [data, data + (n-1)*stride + len) must not wrap the address space
-  if (n > 1 && stride > (UINT64_MAX - (uint64_t)(uintptr_t)data - len) / (n - 1)) return YU_EINVAL;
-  // fill: packets must start 4-byte aligned (no dword shared with a
-  // neighbour's field)
-  if (fill && (((uintptr_t)data | stride) & 3u)) return YU_EINVAL;
+  if (n > 1 && stride > (UINT64_MAX - (uint64_t)(uintptr_t)data - len) / (n - 1))
+    return YU_EINVAL;  // EINVAL:span
+  // fill: packets must start 4-byte aligned. The uniform writers (k_tiny's and
+  // k_lane's write-back, k_small) store whole dwords of each packet's window,
+  // so no dword may hold bytes of two packets.
+  if (fill && (((uintptr_t)data | stride) & 3u)) return YU_EINVAL;  // EINVAL:fill-align
   BatchArgs A;
   A.data = data;
   A.offsets = nullptr;
@@ -2650,7 +2653,8 @@ int batch_ragged(const uint8_t *data, uint8_t *fill, const uint64_t *offsets,
   int rc = check_common(mode, initial_arr, addrs, out, fill != nullptr);
   if (rc) return rc;
   if (n == 0) return YU_OK;
-  if (!offsets || !aligned(offsets, 8) || !data) return YU_EINVAL;
+  if (!offsets || !aligned(offsets, 8)) return YU_EINVAL;  // EINVAL:offsets
+  if (!data) return YU_EINVAL;                             // EINVAL:data
   BatchArgs A;
   A.data = data;
   A.offsets = offsets;
@@ -2708,7 +2712,7 @@ int yu_csum_fill_uniform(uint8_t *data, uint64_t stride, uint32_t len,
                          uint64_t n, int mode, const uint16_t *initial_arr,
                          uint16_t initial, const uint8_t *addrs, uint16_t *out,
                          void *stream) {
-  if (n > 1 && stride < len) return YU_EINVAL;  // overlapping packets
+  if (n > 1 && stride < len) return YU_EINVAL;  // EINVAL:fill-overlap (overlapping packets)
   return batch_uniform(data, data, stride, len, n, mode, initial_arr, initial,
                        addrs, out, stream);
 }
@@ -2717,8 +2721,9 @@ int yu_csum_fill_ragged(uint8_t *data, const uint64_t *offsets, uint64_t n,
                         int mode, const uint16_t *initial_arr,
                         uint16_t initial, const uint8_t *addrs, uint16_t *out,
                         void *stream) {
-  // contract (include/yucsum.h): offsets are multiples of 4, data 4-aligned
-  if ((uintptr_t)data & 3u) return YU_EINVAL;
+  // Any alignment (include/yucsum.h): the ragged writers store each field as one
+  // 16-bit store (even address) or two byte stores, and the TXW kind's whole-line
+  // write-back stores only 128-byte lines that lie inside its own chunk's packets.
   return batch_ragged(data, data, offsets, n, mode, initial_arr, initial,
                       addrs, out, stream);
 }
