@@ -95,7 +95,7 @@ class Workload:
             # 12: config 11 written in place, the burst tundev writes
             #     (network/ipv4/ipv4.go:94 + transport/tcp/connect.go:583, then
             #     link/tundev/tundev.go:171-196): lengths rounded up to 4 B (the
-            #     fill contract: 4-aligned offsets)
+            #     shape rounds 4-5 measure; the writer itself takes any alignment)
             # 13: 1M sendUDP datagrams U{40..200} B back to back, field in place
             #     (header/udp.go:60-62), 4-aligned like 12
             self.mode = {4: batch.RAW, 11: batch.TX_DATAGRAM, 12: batch.TX_DATAGRAM,
@@ -421,9 +421,62 @@ def end_to_end(w: Workload, reps: int = 3):
         for _ in range(k):
             batch.checksum_host_ragged(blob, offs, "tx_datagram", fill=True)
         res[f"tx_burst{bn}_pinned_us_per_call"] = round((time.perf_counter() - t0) / k * 1e6, 1)
+    res["crossover"] = burst_crossover()
     ndev = torch.cuda.device_count()
     if ndev > 1:  # yu_csum_batch_host_uniform_multi: one shard per visible GPU, each on its own PCIe link
         res.update(host_multi_isolated(w.cfg, list(range(ndev))))
+    return res
+
+
+CROSSOVER_BURSTS = (1, 8, 64, 256, 1024)
+
+
+def burst_crossover(L: int = 1500) -> dict:
+    """When does batching pay for a caller holding host packets? The reference hands
+    up one datagram per tundev dispatch (link/tundev/tundev.go:78-114) and sums it on
+    the calling goroutine. Measured here, on one core of this host:
+    * the product's own scalar drop-in, yu_checksum (the Go shim's Checksum for
+      buffers >= 256 B), over one large buffer: its byte rate, and from it the cost of
+      one L-byte packet (a C caller adds ~2 ns per call, a cgo caller ~100 ns);
+    * the batched host path, yu_csum_batch_host_ragged (BatchHostRagged in Go), RAW
+      mode (Checksum(pkt, initial) per packet) on bursts of L-byte packets packed back
+      to back, per call, from pageable memory (a Go heap buffer) and from pinned;
+    * the burst size above which one batched call beats that many scalar calls: from
+      the least-squares line t(k) = a + b*k through the measured bursts, k* = a / (s - b)
+      where s is the scalar cost of one packet (None if the line never crosses)."""
+    L_ = batch.lib()
+    big = np.random.default_rng(3).integers(0, 256, size=256 << 20, dtype=np.uint8)
+    p = big.ctypes.data
+    L_.yu_checksum(p, big.size, 0)  # warm: page faults, caches
+    reps, t0 = 0, time.perf_counter()
+    while reps < 3 or time.perf_counter() - t0 < 0.5:
+        L_.yu_checksum(p, big.size, 0)
+        reps += 1
+    scalar_bps = reps * big.size / (time.perf_counter() - t0)
+    s_us = L / scalar_bps * 1e6
+    res = {"scalar_yu_checksum_GiB_s_1core": round(scalar_bps / GIB, 2),
+           "scalar_us_per_packet": round(s_us, 4), "packet_bytes": L, "bursts": list(CROSSOVER_BURSTS)}
+    rng = np.random.default_rng(11)
+    nmax = max(CROSSOVER_BURSTS)
+    blob_np = rng.integers(0, 256, size=nmax * L, dtype=np.uint8)
+    blob_pin = torch.from_numpy(blob_np.copy()).pin_memory()
+    init = rng.integers(0, 65536, size=nmax, dtype=np.uint16)
+    for kind, blob in (("pageable", blob_np), ("pinned", blob_pin)):
+        us = []
+        for k in CROSSOVER_BURSTS:
+            offs = np.arange(k + 1, dtype=np.uint64) * L
+            o = np.empty(k, np.uint16)
+            for _ in range(10):
+                batch.checksum_host_ragged(blob, offs, "raw", initial_arr=init[:k], out=o)
+            n = 300
+            t0 = time.perf_counter()
+            for _ in range(n):
+                batch.checksum_host_ragged(blob, offs, "raw", initial_arr=init[:k], out=o)
+            us.append((time.perf_counter() - t0) / n * 1e6)
+        b, a = np.polyfit(np.array(CROSSOVER_BURSTS, float), np.array(us), 1)
+        res[f"host_ragged_{kind}_us_per_call"] = [round(u, 2) for u in us]
+        res[f"host_ragged_{kind}_fit_us"] = {"fixed": round(float(a), 2), "per_packet": round(float(b), 4)}
+        res[f"crossover_packets_{kind}"] = round(float(a / (s_us - b)), 1) if s_us > b else None
     return res
 
 

@@ -303,8 +303,9 @@ int yu_csum_fill_ragged(uint8_t *data, const uint64_t *offsets, uint64_t n,
  * pointer (pageable or pinned). The batch is cut into slices that are
  * staged through library-owned pinned buffers on `device` and pipelined
  * (H2D of slice k+1 overlaps the kernel of slice k and the D2H of slice
- * k-1). Synchronous: returns when h_out is complete. Thread-safe (one
- * staging context per calling thread and device). */
+ * k-1). Synchronous: returns when h_out is complete. Thread-safe: each call
+ * borrows one staging context of `device` from a bounded pool and returns it
+ * (see yu_host_staging_bytes below). */
 int yu_csum_batch_host_uniform(const uint8_t *h_data, uint64_t stride,
                                uint32_t len, uint64_t n, int mode,
                                const uint16_t *h_initial_arr,
@@ -384,6 +385,45 @@ int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t *first_iov,
                                  const uint16_t *h_initial_arr,
                                  uint16_t initial, const uint8_t *h_addrs,
                                  uint16_t *h_out, const int *devices, int ndev);
+
+/* ------------------------------------------------------------------ */
+/* Host-path staging (the yu_csum_batch_host_* / yu_csum_fill_host_*   */
+/* calls, and each shard of the _multi forms).                          */
+/* ------------------------------------------------------------------ */
+
+/* A host call borrows one staging context of its device for its own length
+ * and returns it; a caller that finds every context in use waits for one.
+ * Contexts are created on first need, up to yu_host_contexts() per device:
+ * YU_HOST_CONTEXTS in the environment (1..64, default 4; a product setting,
+ * read without the YU_TUNING gate). So the staging grows with the calls the
+ * pool lets run at once, not with the number of OS threads that ever called
+ * (the Go consumer calls from many goroutines, which migrate across OS
+ * threads: transport/tcp/accept.go:238, transport/tcp/endpoint.go:229,
+ * network/ipv4/icmp.go:30-34).
+ *
+ * A context holds 3 pipeline slots of at most one slice each: up to
+ * YU_HOST_SLICE_BYTES of packet bytes and YU_HOST_SLICE_PACKETS packets'
+ * side arrays. Between calls a device's staging is therefore at most
+ * yu_host_contexts() * YU_HOST_CONTEXT_PINNED_MAX bytes of pinned host memory
+ * and yu_host_contexts() * YU_HOST_CONTEXT_DEVICE_MAX of device memory (a
+ * packet longer than a slice gets a slice of its own for that call; the
+ * context gives the extra back when the call returns). */
+#define YU_HOST_SLICE_BYTES (32ull << 20)
+#define YU_HOST_SLICE_PACKETS (1ull << 18)
+#define YU_HOST_CONTEXT_PINNED_MAX \
+  (3ull * (YU_HOST_SLICE_BYTES + 26ull * YU_HOST_SLICE_PACKETS + 72ull))
+#define YU_HOST_CONTEXT_DEVICE_MAX \
+  (3ull * (YU_HOST_SLICE_BYTES + 22ull * YU_HOST_SLICE_PACKETS + 8ull))
+
+/* The pool bound K (YU_HOST_CONTEXTS, clamped to 1..64). */
+int yu_host_contexts(void);
+/* Pinned host bytes the host-path staging of `device` holds now (idle and
+ * lent contexts); the device bytes go to *dev_bytes when it is not NULL.
+ * 0 for a device never used or out of range. Never fails. */
+uint64_t yu_host_staging_bytes(int device, uint64_t *dev_bytes);
+/* Frees the staging of every idle context of `device` (a later call
+ * allocates again). YU_ENODEV for a device out of range. */
+int yu_host_staging_trim(int device);
 
 /* ------------------------------------------------------------------ */
 /* Introspection.                                                      */

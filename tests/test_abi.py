@@ -351,3 +351,23 @@ def test_each_documented_einval_is_returned():
 
 
 YU_MODE_COUNT = 10
+
+
+def test_host_staging_pool_bound_and_setting():
+    """The host path's context pool (include/yucsum.h, Host-path staging): K from
+    YU_HOST_CONTEXTS (default 4, clamped to 1..64, read without the tuning gate), no
+    staging before a first call, the per-context bounds as the header states them."""
+    L = _lib.lib()
+    assert L.yu_host_staging_bytes(0, None) == 0 and L.yu_host_staging_bytes(-1, None) == 0
+    assert L.yu_host_staging_trim(64) == _lib.YU_ENODEV
+    src = open(HEADER).read()
+    assert "#define YU_HOST_SLICE_BYTES (32ull << 20)" in src and "#define YU_HOST_SLICE_PACKETS (1ull << 18)" in src
+    assert _lib.HOST_CONTEXT_PINNED_MAX == 3 * ((32 << 20) + 26 * (1 << 18) + 72)  # ~115.5 MiB
+    probe = f"import sys; sys.path.insert(0, {ROOT!r}); from yustack_amd import _lib; print(_lib.lib().yu_host_contexts())"
+    for val, want in ((None, 4), ("2", 2), ("0", 1), ("100", 64), ("junk", 4)):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("YU_")}
+        if val is not None:
+            env["YU_HOST_CONTEXTS"] = val
+        r = subprocess.run([__import__("sys").executable, "-c", probe], env=env, capture_output=True, text=True,
+                           timeout=60)
+        assert r.returncode == 0 and int(r.stdout) == want, (val, r.stdout, r.stderr)

@@ -1,0 +1,123 @@
+"""The host path's bounded staging (include/yucsum.h, "Host-path staging"): many OS
+threads calling at once — as a Go consumer does from goroutines that migrate across
+threads (transport/tcp/accept.go:238, transport/tcp/endpoint.go:229,
+network/ipv4/icmp.go:30-34) — share at most yu_host_contexts() contexts per device,
+every result stays bit-exact against the oracle, and the pinned and device staging
+stays within the documented bound."""
+import os
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from yustack_amd import _lib, batch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _tcp_batch(rng, n, L=1500):
+    b = rng.integers(0, 256, size=n * L, dtype=np.uint8)
+    b.reshape(n, L)[:, 12] = 0x50
+    return b, rng.integers(0, 256, size=8 * n, dtype=np.uint8)
+
+
+def test_many_threads_share_a_bounded_pool(dev, oracle_c):
+    """64 threads at once: 12 make large pageable calls (48 MiB, so pipelined over
+    several 32 MiB slices), 12 large ragged RAW calls, 40 make small bursts (64 x 1500
+    B: the direct path). Three rounds each. Every result equals the oracle's, at most
+    K contexts were ever created, and the staging held afterwards is within K times
+    the per-context bound; trimming gives it back."""
+    rng = np.random.default_rng(64)
+    K = _lib.lib().yu_host_contexts()
+    assert 1 <= K <= 64
+    big_n = (48 << 20) // 1500
+    big, big_a = _tcp_batch(rng, big_n)
+    big_want = oracle_c.batch(big, O.MODE_TCP, stride=1500, length=1500, n=big_n, addrs=big_a, threads=8)
+    lens = rng.integers(64, 9001, size=9000)
+    offs = np.zeros(lens.size + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    rag = rng.integers(0, 256, size=int(offs[-1]), dtype=np.uint8)
+    rag_i = rng.integers(0, 65536, size=lens.size, dtype=np.uint16)
+    rag_want = oracle_c.batch(rag, O.MODE_RAW, offsets=offs, initial_arr=rag_i, threads=8)
+    small = [_tcp_batch(rng, 64) for _ in range(4)]
+    small_want = [oracle_c.batch(b, O.MODE_TCP, stride=1500, length=1500, n=64, addrs=a) for b, a in small]
+
+    errors = []
+    start = threading.Barrier(64)
+
+    def work(kind, k):
+        try:
+            start.wait()
+            for _ in range(3):
+                if kind == "big":
+                    got = batch.checksum_host_uniform(big, 1500, 1500, big_n, "tcp", addrs=big_a)
+                    ok = np.array_equal(got, big_want)
+                elif kind == "rag":
+                    got = batch.checksum_host_ragged(rag, offs, "raw", initial_arr=rag_i)
+                    ok = np.array_equal(got, rag_want)
+                else:
+                    b, a = small[k % 4]
+                    got = batch.checksum_host_uniform(b, 1500, 1500, 64, "tcp", addrs=a)
+                    ok = np.array_equal(got, small_want[k % 4])
+                if not ok:
+                    errors.append((kind, k))
+        except Exception as e:  # noqa: BLE001 — reported below
+            errors.append((kind, k, repr(e)))
+
+    kinds = ["big"] * 12 + ["rag"] * 12 + ["small"] * 40
+    threads = [threading.Thread(target=work, args=(kd, k)) for k, kd in enumerate(kinds)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in threads), "host calls did not finish"
+    assert not errors, errors[:5]
+    pinned, devb = _lib.host_staging(0)
+    print(f"K={K}: staging after 64 threads: pinned {pinned / 2**20:.1f} MiB, device {devb / 2**20:.1f} MiB")
+    assert 0 < pinned <= K * _lib.HOST_CONTEXT_PINNED_MAX
+    assert 0 < devb <= K * _lib.HOST_CONTEXT_DEVICE_MAX
+    assert _lib.lib().yu_host_staging_trim(0) == 0
+    assert _lib.host_staging(0) == (0, 0)
+    # the pool still serves calls after a trim
+    b, a = small[0]
+    assert np.array_equal(batch.checksum_host_uniform(b, 1500, 1500, 64, "tcp", addrs=a), small_want[0])
+    assert _lib.lib().yu_host_staging_trim(64) == _lib.YU_ENODEV
+
+
+_ONE_CONTEXT = r"""
+import sys, threading
+sys.path.insert(0, %r)
+import numpy as np
+from yustack_amd import _lib, batch
+from oracle import oracle as O
+assert _lib.lib().yu_host_contexts() == 1
+rng = np.random.default_rng(7)
+n = 40000
+b = rng.integers(0, 256, size=n * 1500, dtype=np.uint8)
+want = O.C().batch(b, O.MODE_RAW, stride=1500, length=1500, n=n, threads=8)
+bad = []
+def go():
+    for _ in range(2):
+        if not np.array_equal(batch.checksum_host_uniform(b, 1500, 1500, n, "raw"), want):
+            bad.append(1)
+ts = [threading.Thread(target=go) for _ in range(8)]
+[t.start() for t in ts]
+[t.join() for t in ts]
+p, d = _lib.host_staging(0)
+assert not bad and 0 < p <= _lib.HOST_CONTEXT_PINNED_MAX and d <= _lib.HOST_CONTEXT_DEVICE_MAX, (bad, p, d)
+print("ok", p, d)
+"""
+
+
+def test_one_context_serialises_callers(dev):
+    """YU_HOST_CONTEXTS=1: eight threads' pipelined calls take turns on the one
+    context (each waits for it), all bit-exact, one context's staging held."""
+    env = dict(os.environ, YU_HOST_CONTEXTS="1")
+    r = subprocess.run([sys.executable, "-c", _ONE_CONTEXT % ROOT], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.startswith("ok")

@@ -23,7 +23,13 @@ EXPORTS = (
     "yu_csum_fill_host_uniform", "yu_csum_fill_host_ragged", "yu_csum_fill_host_iov",
     "yu_abi_version", "yu_strerror", "yu_device_count", "yu_uniform_variant", "yu_uniform_variant_n",
     "yu_ragged_variant", "yu_ragged_variant_n", "yu_ragged_fill_variant_n",
+    "yu_host_contexts", "yu_host_staging_bytes", "yu_host_staging_trim",
 )
+
+# Host-path staging bounds (include/yucsum.h): per context, between calls.
+HOST_SLICE_BYTES, HOST_SLICE_PACKETS = 32 << 20, 1 << 18
+HOST_CONTEXT_PINNED_MAX = 3 * (HOST_SLICE_BYTES + 26 * HOST_SLICE_PACKETS + 72)
+HOST_CONTEXT_DEVICE_MAX = 3 * (HOST_SLICE_BYTES + 22 * HOST_SLICE_PACKETS + 8)
 
 YU_OK, YU_EINVAL, YU_ENODEV, YU_ENOMEM, YU_EHIP_BASE = 0, -22, -19, -12, -1000
 
@@ -102,6 +108,12 @@ def lib() -> ctypes.CDLL:
     L.yu_ragged_variant_n.argtypes = [i32, u64]
     L.yu_ragged_fill_variant_n.restype = c.c_char_p
     L.yu_ragged_fill_variant_n.argtypes = [i32, u64]
+    L.yu_host_contexts.restype = i32
+    L.yu_host_contexts.argtypes = []
+    L.yu_host_staging_bytes.restype = u64
+    L.yu_host_staging_bytes.argtypes = [i32, vp]
+    L.yu_host_staging_trim.restype = i32
+    L.yu_host_staging_trim.argtypes = [i32]
     del u8
     _lib = L
     return L
@@ -117,3 +129,11 @@ def strerror(status: int) -> str:
 def check(status: int, what: str) -> None:
     if status != YU_OK:
         raise YuError(status, what)
+
+
+def host_staging(device: int = 0) -> tuple[int, int]:
+    """(pinned host bytes, device bytes) the host-path staging of `device` holds now
+    (yu_host_staging_bytes); both 0 before its first host call."""
+    d = ctypes.c_uint64(0)
+    pinned = lib().yu_host_staging_bytes(device, ctypes.byref(d))
+    return int(pinned), int(d.value)

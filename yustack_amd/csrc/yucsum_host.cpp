@@ -17,9 +17,14 @@
 // slot while the previous slices are on the GPU. A batch of at most 4 MiB
 // (a tun read burst) skips the copies instead: the kernel reads the pinned
 // host memory and writes the results there over PCIe (see `direct`), which
-// more than halves the per-call latency. Staging buffers are per
-// (calling thread, device) and grow on demand; nothing is shared between
-// threads, so concurrent callers need no lock.
+// more than halves the per-call latency. Staging lives in a bounded per-device
+// pool of contexts (ContextPool: at most YU_HOST_CONTEXTS of them, default 4,
+// each 3 slots of at most one slice), checked out for the length of one call and
+// returned: concurrent callers share nothing while they hold one, and a caller
+// that finds every context of its device in use waits for one. Memory therefore
+// grows with the number of concurrent calls the pool allows, not with the
+// number of OS threads that ever called (a Go caller's goroutines migrate over
+// many of them); yu_host_staging_bytes reports it.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -27,6 +32,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -42,7 +48,12 @@
 namespace {
 
 constexpr int kSlots = 3;
-constexpr uint64_t kSliceBytes = 32ull << 20;
+constexpr uint64_t kSliceBytes = YU_HOST_SLICE_BYTES;  // 32 MiB
+// Packets per slice at most: bounds a slot's side arrays (34 bytes of pinned and
+// 30 of device memory per packet) as kSliceBytes bounds its packet bytes. Only
+// packets under 128 bytes reach it; 256K of 64-byte packets is 16 MiB, still
+// hundreds of microseconds of PCIe per slice.
+constexpr uint64_t kSlicePkts = YU_HOST_SLICE_PACKETS;  // 256K
 
 int hip_rc(hipError_t e) {
   if (e == hipSuccess) return YU_OK;
@@ -74,9 +85,24 @@ struct Slot {
   bool busy = false, staged_out = false;
 };
 
+// Staging bytes of a context reserved for (data_bytes, pk): pinned host and device.
+// (the allocations of Ctx::reserve: packet bytes, addrs 8, initial 2, results 4,
+// offsets 8, coherent results 4 per packet, one more offset, the 64-byte flag)
+constexpr uint64_t pinned_bytes(uint64_t data_bytes, uint64_t pk) {
+  return kSlots * ((data_bytes ? data_bytes : 16) + pk * 8 + pk * 2 + pk * 4 + (pk + 1) * 8 + pk * 4 + 64);
+}
+constexpr uint64_t device_bytes(uint64_t data_bytes, uint64_t pk) {
+  return kSlots * ((data_bytes ? data_bytes : 16) + pk * 8 + pk * 2 + pk * 4 + (pk + 1) * 8);
+}
+static_assert(pinned_bytes(kSliceBytes, kSlicePkts) == YU_HOST_CONTEXT_PINNED_MAX, "yucsum.h bound");
+static_assert(device_bytes(kSliceBytes, kSlicePkts) == YU_HOST_CONTEXT_DEVICE_MAX, "yucsum.h bound");
+static_assert(kSlots == 3, "yucsum.h bounds assume 3 slots");
+
 struct Ctx {
   int dev = -1;
-  uint64_t cap_data = 0, cap_pk = 0;
+  // (atomic: yu_host_staging_bytes reads them while the holder may reserve)
+  std::atomic<uint64_t> cap_data{0}, cap_pk{0};
+  std::atomic<bool> reserved{false};
   Slot s[kSlots];
 
   void release() {
@@ -98,6 +124,7 @@ struct Ctx {
       x = Slot();
     }
     cap_data = cap_pk = 0;
+    reserved = false;
   }
   ~Ctx() {
     if (dev >= 0 && hipSetDevice(dev) == hipSuccess) release();
@@ -108,6 +135,7 @@ struct Ctx {
     if (data_bytes < cap_data) data_bytes = cap_data;
     if (pk < cap_pk) pk = cap_pk;
     release();
+    reserved = true;  // (partly) allocated: release() frees what a failure left
     for (Slot &x : s) {
       YU_TRY(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
       YU_TRY(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
@@ -132,7 +160,81 @@ struct Ctx {
   }
 };
 
-thread_local std::unique_ptr<Ctx> t_ctx[64];
+// Upper bound on the staging contexts of one device (YU_HOST_CONTEXTS, 1..64,
+// default 4): a product setting, like the reference's tundev.BufConfig
+// (link/tundev/tundev.go:20), not a measurement knob, so it is read without the
+// YU_TUNING gate.
+int host_contexts() {
+  static const int v = [] {
+    const char *e = getenv("YU_HOST_CONTEXTS");
+    char *end = nullptr;
+    const long k = e && *e ? strtol(e, &end, 10) : 4;
+    if (e && *e && *end) return 4;  // not a number: the default
+    return (int)(k < 1 ? 1 : (k > 64 ? 64 : k));
+  }();
+  return v;
+}
+
+// The bounded context pool of one device. Contexts are created lazily, up to
+// host_contexts(), and live for the process (never destroyed at exit, when the
+// HIP runtime may already be gone); an idle one is lent to the next caller.
+class ContextPool {
+ public:
+  Ctx *acquire(int dev) {
+    std::unique_lock<std::mutex> l(m_);
+    cv_.wait(l, [&] { return !idle_.empty() || (int)all_.size() < host_contexts(); });
+    Ctx *c;
+    if (!idle_.empty()) {
+      c = idle_.back();
+      idle_.pop_back();
+    } else {
+      all_.push_back(new Ctx());
+      c = all_.back();
+      c->dev = dev;
+    }
+    return c;
+  }
+  // A context that grew past one standard slice (a packet longer than
+  // kSliceBytes is a slice of its own) gives that memory back here, so the pool
+  // keeps at most host_contexts() x one standard slot budget between calls.
+  void give_back(Ctx *c) {
+    if (c->cap_data > kSliceBytes || c->cap_pk > kSlicePkts) c->release();
+    {
+      std::lock_guard<std::mutex> l(m_);
+      idle_.push_back(c);
+    }
+    cv_.notify_one();
+  }
+  // Staging held right now by this device's contexts (idle and lent).
+  void held(uint64_t &pinned, uint64_t &dev) {
+    std::lock_guard<std::mutex> l(m_);
+    pinned = dev = 0;
+    for (Ctx *c : all_) {
+      if (!c->reserved) continue;
+      pinned += pinned_bytes(c->cap_data, c->cap_pk);
+      dev += device_bytes(c->cap_data, c->cap_pk);
+    }
+  }
+  // Frees the staging of every idle context (lent ones are left alone).
+  void trim() {
+    std::lock_guard<std::mutex> l(m_);
+    for (Ctx *c : idle_) c->release();
+  }
+  int created() {
+    std::lock_guard<std::mutex> l(m_);
+    return (int)all_.size();
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::vector<Ctx *> all_, idle_;
+};
+
+ContextPool &pool_of(int device) {
+  static ContextPool *pools = new ContextPool[64];  // process lifetime
+  return pools[device];
+}
 
 // Staging copies of pageable input. One thread's memcpy into pinned memory
 // runs at roughly half the PCIe rate, so a 32 MiB slice is split across a small
@@ -245,21 +347,27 @@ int finish(Slot &x, uint16_t *h_out) {
   return YU_OK;
 }
 
-Ctx &context(int device) {
-  std::unique_ptr<Ctx> &cp = t_ctx[device];
-  if (!cp) {
-    cp.reset(new Ctx());
-    cp->dev = device;
+// A context of `device` for the length of one call (RAII: returned to the pool
+// on every exit path).
+class Lease {
+ public:
+  explicit Lease(int device) : device_(device), c_(pool_of(device).acquire(device)) {
+    // A previous call that failed midway may have left slices in flight:
+    // drain them without copying (their h_out belonged to that call).
+    for (Slot &x : c_->s) {
+      if (x.busy) (void)hipEventSynchronize(x.done);
+      x.busy = false;
+    }
   }
-  Ctx &c = *cp;
-  // A previous call that failed midway may have left slices in flight:
-  // drain them without copying (their h_out belonged to that call).
-  for (Slot &x : c.s) {
-    if (x.busy) (void)hipEventSynchronize(x.done);
-    x.busy = false;
-  }
-  return c;
-}
+  ~Lease() { pool_of(device_).give_back(c_); }
+  Lease(const Lease &) = delete;
+  Lease &operator=(const Lease &) = delete;
+  Ctx &ctx() { return *c_; }
+
+ private:
+  int device_;
+  Ctx *c_;
+};
 
 // Small batches (a tun read burst) go "direct": the kernel reads the pinned
 // host bytes and side arrays and writes the results over PCIe itself — one
@@ -452,7 +560,7 @@ struct UniformLayout {
 template <class Span>
 uint64_t byte_slice(uint64_t first, uint64_t n, const Span &span) {
   uint64_t cnt = 0, b = 0;
-  while (first + cnt < n) {
+  while (first + cnt < n && cnt < kSlicePkts) {
     const uint64_t l = span(first + cnt);
     if (cnt && b + l > kSliceBytes) break;
     b += l;
@@ -556,7 +664,11 @@ int on_device(int device, F &&f) {
   int prev = 0;
   YU_TRY(hipGetDevice(&prev));
   YU_TRY(hipSetDevice(device));
-  int rc = f(context(device));
+  int rc;
+  {
+    Lease lease(device);
+    rc = f(lease.ctx());
+  }
   (void)hipSetDevice(prev);
   return rc;
 }
@@ -719,6 +831,7 @@ extern "C" int yu_csum_batch_host_uniform(const uint8_t *h_data,
   return on_device(device, [&](Ctx &c) {
     const uint64_t pstride = stride ? stride : 1;
     uint64_t slice = kSliceBytes / pstride;
+    if (slice > kSlicePkts) slice = kSlicePkts;
     if (slice < 1) slice = 1;
     if (slice > n) slice = n;
     UniformLayout L{h_data, stride, n, slice, len, mode, initial, is_pinned(h_data)};
@@ -824,6 +937,28 @@ extern "C" int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t 
                                   h_initial_arr ? h_initial_arr + a : nullptr, initial,
                                   h_addrs ? h_addrs + 8 * a : nullptr, h_out + a * YU_MODE_OUTPUTS(mode), devices[i]);
   });
+}
+
+extern "C" uint64_t yu_host_staging_bytes(int device, uint64_t *dev_bytes) {
+  uint64_t pinned = 0, dev = 0;
+  if (device >= 0 && device < 64) pool_of(device).held(pinned, dev);
+  if (dev_bytes) *dev_bytes = dev;
+  return pinned;
+}
+
+extern "C" int yu_host_contexts(void) { return host_contexts(); }
+
+extern "C" int yu_host_staging_trim(int device) {
+  if (device < 0 || device >= 64) return YU_ENODEV;
+  int prev = 0;
+  const bool restore = hipGetDevice(&prev) == hipSuccess;
+  if (hipSetDevice(device) != hipSuccess) {
+    (void)hipGetLastError();
+    return YU_ENODEV;
+  }
+  pool_of(device).trim();
+  if (restore) (void)hipSetDevice(prev);
+  return YU_OK;
 }
 
 // ---------------------------------------------------------------------
