@@ -1,9 +1,17 @@
-# round 4, last calls: the final tree verified as the driver runs it (GPU suite,
-# smoke, default bench line: tools/verify_round.sh) plus the driver-settings line.
-#   gpurun --timeout 1200 -- 'bash tools/gpu_step.sh r04f'
+# scratch: the GPU step of the current session's latest gpurun call (round 5).
+# The suite runs to the end unless it dies (test failures are read from the log;
+# a fault, abort, signal or time limit ends the call), then smoke() and the default
+# bench line, each under its own time limit.
+#   gpurun --timeout 1200 -- 'bash tools/gpu_step.sh r05a'
 set -o pipefail
-TAG=${1:-final}
+TAG=${1:-r05}
 mkdir -p gpurun_out
-bash tools/verify_round.sh $TAG || exit 1
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${TAG}_driver.json 2> gpurun_out/bench_${TAG}_driver.err || { tail gpurun_out/bench_${TAG}_driver.err; exit 1; }
-echo bench-ok
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=8 -rf --timeout 240 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
+rc=$?
+tail -15 gpurun_out/gpu_tests_$TAG.log
+[ $rc -le 1 ] || { echo "pytest rc $rc: stopping"; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail gpurun_out/smoke_$TAG.log; exit 1; }
+tail -1 gpurun_out/smoke_$TAG.log
+timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail gpurun_out/bench_$TAG.err; exit 1; }
+echo "bench ok; pytest rc $rc"
+exit $rc
