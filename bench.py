@@ -428,7 +428,7 @@ def end_to_end(w: Workload, reps: int = 3):
     return res
 
 
-CROSSOVER_BURSTS = (1, 8, 64, 256, 1024)
+CROSSOVER_BURSTS = (1, 8, 64, 256, 1024, 4096, 16384)
 
 
 def burst_crossover(L: int = 1500) -> dict:
@@ -441,9 +441,12 @@ def burst_crossover(L: int = 1500) -> dict:
     * the batched host path, yu_csum_batch_host_ragged (BatchHostRagged in Go), RAW
       mode (Checksum(pkt, initial) per packet) on bursts of L-byte packets packed back
       to back, per call, from pageable memory (a Go heap buffer) and from pinned;
-    * the burst size above which one batched call beats that many scalar calls: from
-      the least-squares line t(k) = a + b*k through the measured bursts, k* = a / (s - b)
-      where s is the scalar cost of one packet (None if the line never crosses)."""
+    * the burst size above which one batched call beats that many scalar calls: the
+      first measured burst where it does, and k* where the straight line through that
+      burst's time and the one before it meets k * s, s being the scalar cost of one
+      packet (None when no measured burst is faster).
+    Bursts up to 4 MiB take the direct path (one launch reading host memory), larger
+    ones the pipelined copies (include/yucsum.h)."""
     L_ = batch.lib()
     big = np.random.default_rng(3).integers(0, 256, size=256 << 20, dtype=np.uint8)
     p = big.ctypes.data
@@ -473,10 +476,20 @@ def burst_crossover(L: int = 1500) -> dict:
             for _ in range(n):
                 batch.checksum_host_ragged(blob, offs, "raw", initial_arr=init[:k], out=o)
             us.append((time.perf_counter() - t0) / n * 1e6)
-        b, a = np.polyfit(np.array(CROSSOVER_BURSTS, float), np.array(us), 1)
         res[f"host_ragged_{kind}_us_per_call"] = [round(u, 2) for u in us]
-        res[f"host_ragged_{kind}_fit_us"] = {"fixed": round(float(a), 2), "per_packet": round(float(b), 4)}
-        res[f"crossover_packets_{kind}"] = round(float(a / (s_us - b)), 1) if s_us > b else None
+        cross = None
+        for j, (k, u) in enumerate(zip(CROSSOVER_BURSTS, us)):
+            if u < k * s_us:
+                if j == 0:
+                    cross = float(k)
+                else:
+                    k0, u0 = CROSSOVER_BURSTS[j - 1], us[j - 1]
+                    slope = (u - u0) / (k - k0)
+                    cross = (u0 - slope * k0) / (s_us - slope)
+                res[f"first_burst_batched_wins_{kind}"] = k
+                break
+        res[f"crossover_packets_{kind}"] = None if cross is None else round(cross, 1)
+    res["scalar_us_per_call_at_bursts"] = [round(k * s_us, 2) for k in CROSSOVER_BURSTS]
     return res
 
 
@@ -618,13 +631,13 @@ def _device_count(env=None, nodes: str = KFD_NODES, dri: str = DRI_DIR) -> int:
     launcher starts its ranks before anything here has touched a GPU: the KFD topology
     nodes that are GPUs (gfx_target_version != 0) and whose render node this process
     can open — the enumeration the ROCm runtime does — then cut by
-    ROCR_VISIBLE_DEVICES (the ROCr layer), then by ONE HIP-level list:
-    HIP_VISIBLE_DEVICES when it is set and non-empty, else CUDA_VISIBLE_DEVICES when
-    that is (HIP reads the CUDA name only as a fallback; an empty value is no list).
-    Opening a render node is a plain DRM file open (no KFD queue, no HIP).
-    tests/test_bench_launch.py checks the parsing on a fake topology;
-    tests/test_gpu_dist.py checks the count against torch.cuda.device_count() for
-    each of these environments, both-set and empty-string ones included."""
+    ROCR_VISIBLE_DEVICES (the ROCr layer; an empty value is no list), then by ONE
+    HIP-level list: HIP_VISIBLE_DEVICES when it is set, else CUDA_VISIBLE_DEVICES when
+    that is; at this level an empty value hides every device. Measured on the MI355X
+    box (profiles/r05/device_count_r05a.txt, tests/test_gpu_dist.py): HIP="" -> 0,
+    CUDA="" -> 0, HIP=0 with CUDA=7 -> 1, HIP=7 with CUDA=0 -> 0, HIP="" with CUDA=0 ->
+    0, ROCR="" -> 1 (of 1). Opening a render node is a plain DRM file open (no KFD
+    queue, no HIP). tests/test_bench_launch.py checks the parsing on a fake topology."""
     env = os.environ if env is None else env
     n = 0
     try:
@@ -651,8 +664,10 @@ def _device_count(env=None, nodes: str = KFD_NODES, dri: str = DRI_DIR) -> int:
             continue  # not ours (not passed into this container, or no permission)
         os.close(fd)
         n += 1
-    n = _visible_cut(n, env.get("ROCR_VISIBLE_DEVICES"))
-    hip_list = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES") or None
+    n = _visible_cut(n, env.get("ROCR_VISIBLE_DEVICES") or None)
+    hip_list = env.get("HIP_VISIBLE_DEVICES")
+    if hip_list is None:
+        hip_list = env.get("CUDA_VISIBLE_DEVICES")
     return _visible_cut(n, hip_list)
 
 

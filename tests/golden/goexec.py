@@ -11,13 +11,25 @@ copied) with Go's semantics for the constructs they use:
 * strings and `[]byte(s)` conversions, `[]byte{...}` literals, `make([]byte, n)`;
 * named slice types with methods (`type TCP []byte`, `func (b TCP) ...`);
 * `const` blocks with `iota`, `:=`, `=`, `op=`, `++`, `--`, `if`, 3-clause `for`,
-  `return`, package-qualified calls across the loaded packages, and
-  `encoding/binary.BigEndian` (stdlib, restated).
+  `for k, v := range`, `return`, package-qualified calls across the loaded packages,
+  and `encoding/binary.BigEndian` (stdlib, restated);
+* struct types (zero values per field type), keyed and positional composite literals,
+  `&T{...}`, pointer receivers, field reads and stores, 3-index slices, slices of
+  non-byte values (`[]header.Network{ipv4}`), function literals (closures over their
+  scope), variadic parameters, and calls through interface values (dispatch on the
+  concrete value, as Go does at run time).
+
+Struct values are shared, not copied, on assignment: the code the path executes never
+copies a struct and then changes both copies. Values from outside the loaded packages
+(a `*testing.T`, a link endpoint, `log.Printf`) are Python stubs the caller supplies.
 
 Function bodies are parsed lazily, when first called, so code the path does not reach
-(struct types, options parsing, ...) is only skipped over. tests/golden/make_golden.py
-uses it to produce known-answer vectors "from the reference itself" for the functions
-on the path (checksum/checksum.go, header/{ipv4,tcp,udp}.go), pinning the C oracle.
+(options parsing, the TCP state machine, ...) is only skipped over.
+tests/golden/make_refexec.py uses it to produce known-answer vectors "from the
+reference itself": checksum/checksum.go, header/{ipv4,tcp,udp,icmpv4}.go, the senders
+(transport/udp/endpoint.go sendUDP, transport/tcp/connect.go sendTCP /
+sendTCPWithOptions, network/ipv4/icmp.go sendICMPv4, network/ipv4/ipv4.go
+WritePacket, types/route.go, buffer/prependable.go) and checker/checker.go.
 """
 from __future__ import annotations
 
@@ -96,6 +108,51 @@ class Str:
         self.b, self.t = bytes(b), t
 
 
+class Struct:
+    """A struct value (or the value a pointer to it points at): fields by name."""
+    __slots__ = ("t", "pkg", "f")
+
+    def __init__(self, t, pkg, fields):
+        self.t, self.pkg, self.f = t, pkg, fields
+
+    def __repr__(self):
+        return f"{self.t}{self.f}"
+
+
+class GoList:
+    """A slice of non-byte values ([]header.Network, variadic parameters)."""
+    __slots__ = ("items", "t")
+
+    def __init__(self, items, t="[]"):
+        self.items, self.t = list(items), t
+
+    @property
+    def len(self):
+        return len(self.items)
+
+    def get(self, i):
+        if not 0 <= i < len(self.items):
+            raise GoPanic(f"index out of range [{i}] with length {len(self.items)}")
+        return self.items[i]
+
+    def set(self, i, x):
+        self.get(i)
+        self.items[i] = x
+
+
+class Closure:
+    """A function literal with the scopes it closes over; `owner` names the function
+    it was created in (for Interp.watch)."""
+    __slots__ = ("params", "body", "env", "pkg", "owner")
+
+    def __init__(self, params, body, env, pkg, owner):
+        self.params, self.body, self.env, self.pkg, self.owner = params, body, env, pkg, owner
+
+
+class GoFatal(Exception):
+    """t.Fatalf from a stub *testing.T: ends the checker, as runtime.Goexit does."""
+
+
 # ----------------------------------------------------------------------------- lexer
 TOK = re.compile(r"""
  (?P<ws>[ \t\r]+) | (?P<nl>\n) | (?P<lc>//[^\n]*) | (?P<bc>/\*.*?\*/)
@@ -139,6 +196,7 @@ PREC = {"||": 1, "&&": 2, "==": 3, "!=": 3, "<": 3, "<=": 3, ">": 3, ">=": 3,
 class Parser:
     def __init__(self, toks, i=0):
         self.t, self.i = toks, i
+        self.nolit = False  # inside an if / for header: `x {` opens the block
 
     def peek(self, k=0):
         return self.t[self.i + k]
@@ -176,18 +234,91 @@ class Parser:
                 if not depth:
                     return
 
-    # --- types (only what the path needs: names, []T, qualified names)
+    # --- types: names, qualified names, []T, [N]T, *T, ...T; map / chan / func /
+    # struct / interface types are skipped over (only their name is kept)
     def parse_type(self):
+        if self.accept("..."):
+            return "..." + self.parse_type()
         if self.accept("["):
+            if self.accept("]"):
+                return "[]" + self.parse_type()
+            n = self.expr()
             self.expect("]")
-            return "[]" + self.parse_type()
+            return "[" + (str(n[1].v) if n[0] == "lit" else "?") + "]" + self.parse_type()
         if self.accept("*"):
             return "*" + self.parse_type()
+        if self.val() == "map":
+            self.next()
+            self.skip_balanced()
+            self.parse_type()
+            return "map"
+        if self.val() == "chan":
+            self.next()
+            self.parse_type()
+            return "chan"
+        if self.val() == "func":
+            self.next()
+            self.skip_balanced()
+            if self.val() == "(":
+                self.skip_balanced()
+            elif self.peek()[0] == "id" or self.val() in ("[", "*"):
+                self.parse_type()
+            return "func"
+        if self.val() in ("struct", "interface"):
+            self.next()
+            self.skip_balanced()
+            return "struct{}"
         name = self.next()[1]
         if self.val() == "." and self.peek(1)[0] == "id":
             self.next()
             name = name + "." + self.next()[1]
         return name
+
+    def struct_fields(self):
+        """`struct { a, b T; C }` after the keyword: [(name, type)]."""
+        self.expect("{")
+        out = []
+        while not self.accept("}"):
+            if self.accept(";"):
+                continue
+            names = [self.next()[1]]
+            while self.accept(","):
+                names.append(self.next()[1])
+            if self.val() in (";", "}") or self.peek()[0] == "str":  # embedded field
+                t = names[0]
+            else:
+                t = self.parse_type()
+            if self.peek()[0] == "str":  # field tag
+                self.next()
+            out += [(nm, t) for nm in names]
+        return out
+
+    def params(self):
+        """A parameter list after its "(": [(name or None, type)]."""
+        params, pending = [], []
+        while not self.accept(")"):
+            if self.peek()[0] != "id" and self.val() not in ("...",):
+                pending.append(self.parse_type())  # unnamed: a type
+                self.accept(",")
+                continue
+            nm = self.next()[1]
+            if self.val() in (",", ")"):
+                pending.append(nm)
+                self.accept(",")
+                continue
+            if self.val() == ".":  # a qualified type with no name
+                self.i -= 1
+                pending.append(self.parse_type())
+                self.accept(",")
+                continue
+            t = self.parse_type()
+            for q in pending + [nm]:
+                params.append((q, t))
+            pending = []
+            self.accept(",")
+        for q in pending:  # unnamed params: types only
+            params.append((None, q))
+        return params
 
     # --- expressions
     def expr(self, prec=1):
@@ -203,7 +334,7 @@ class Parser:
 
     def unary(self):
         v = self.val()
-        if self.peek()[0] == "op" and v in ("-", "+", "!", "^"):
+        if self.peek()[0] == "op" and v in ("-", "+", "!", "^", "&", "*"):
             self.next()
             return ("un", v, self.unary())
         return self.primary()
@@ -232,12 +363,24 @@ class Parser:
                 x = ("slicelit", t, elems)
             else:
                 x = ("name", t)
+        elif v == "func":  # function literal
+            self.expect("(")
+            params = self.params()
+            while self.val() != "{":
+                if self.val() == "(":
+                    self.skip_balanced()
+                else:
+                    self.parse_type()
+            x = ("funclit", params, self.block())
         elif kind == "id":
             x = ("name", v)
         else:
             raise SyntaxError(f"unexpected {v!r}")
         while True:
             v = self.val()
+            if v == "{" and not self.nolit and self._typeish(x):  # composite literal
+                x = ("complit", x, self.complit_body())
+                continue
             if v == ".":
                 self.next()
                 x = ("sel", x, self.next()[1])
@@ -252,23 +395,47 @@ class Parser:
                 self.next()
                 lo = None if self.val() == ":" else self.expr()
                 if self.accept(":"):
-                    hi = None if self.val() == "]" else self.expr()
+                    hi = None if self.val() in ("]", ":") else self.expr()
+                    mx = self.expr() if self.accept(":") else None
                     self.expect("]")
-                    x = ("slice", x, lo, hi)
+                    x = ("slice", x, lo, hi, mx)
                 else:
                     self.expect("]")
                     x = ("index", x, lo)
             else:
                 return x
 
-    # --- statements
-    def block(self):
+    @staticmethod
+    def _typeish(x):
+        """A composite literal's type: a name starting with a capital or lower letter
+        that is a type (resolved at run time), or pkg.Name."""
+        return x[0] == "name" and not x[1].startswith("[]") or (x[0] == "sel" and x[1][0] == "name")
+
+    def complit_body(self):
+        """`{k: v, ...}` or `{v, ...}`: [(key or None, expr)]."""
         self.expect("{")
         out = []
         while not self.accept("}"):
             if self.accept(";"):
                 continue
+            e = self.expr()
+            if self.accept(":"):
+                out.append((e[1], self.expr()))
+            else:
+                out.append((None, e))
+            self.accept(",")
+        return out
+
+    # --- statements
+    def block(self):
+        self.expect("{")
+        saved, self.nolit = self.nolit, False
+        out = []
+        while not self.accept("}"):
+            if self.accept(";"):
+                continue
             out.append(self.stmt())
+        self.nolit = saved
         return out
 
     def simple(self):
@@ -300,9 +467,11 @@ class Parser:
         if v == "if":
             self.next()
             init = None
+            self.nolit = True
             s = self.simple()
             if self.accept(";"):
                 init, s = s, self.simple()
+            self.nolit = False
             body = self.block()
             els = None
             if self.accept("else"):
@@ -311,6 +480,21 @@ class Parser:
         if v == "for":
             self.next()
             init = cond = post = None
+            self.nolit = True
+            j = self.i  # `for k, v := range x {`
+            while self.t[j][1] not in ("{", ";", "range"):
+                j += 1
+            if self.t[j][1] == "range":
+                keys = [] if self.val() == "range" else [self.expr()]
+                while self.accept(","):
+                    keys.append(self.expr())
+                define = self.accept(":=")
+                if not define:
+                    self.accept("=")
+                self.expect("range")
+                x = self.expr()
+                self.nolit = False
+                return ("range", keys, define, x, self.block())
             if self.val() != "{":
                 s = self.simple()
                 if self.accept(";"):
@@ -320,6 +504,7 @@ class Parser:
                     post = None if self.val() == "{" else self.simple()
                 else:
                     cond = s[1]
+            self.nolit = False
             return ("for", init, cond, post, self.block())
         if v == "var":
             self.next()
@@ -345,6 +530,7 @@ class Package:
     def __init__(self, name):
         self.name = name
         self.funcs, self.methods, self.consts, self.types, self.imports = {}, {}, {}, {}, {}
+        self.structs = {}  # name -> [(field, type)]
 
 
 class Return(Exception):
@@ -357,6 +543,12 @@ class Interp:
 
     def __init__(self, root, module="github.com/YaoZengzeng/yustack"):
         self.root, self.module, self.pkgs = root, module, {}
+        # packages outside the loaded tree, as Python callables: "pkg.Func" -> f(*args)
+        self.stubs = {"log.Printf": lambda *a: None, "log.Println": lambda *a: None}
+        # functions whose locals to keep when they return (or end in a panic / Fatalf):
+        # (package, name) or (package, "Outer.func") for a function literal in Outer
+        self.watch, self.frames = set(), {}
+        self._fn_stack = []  # names of the functions being run (a literal's owner)
 
     def load(self, rel_dir, files=None):
         d = os.path.join(self.root, rel_dir)
@@ -402,7 +594,10 @@ class Interp:
                     p.next()
                     p.next()
                     pkg.types[tname] = "[]" + p.parse_type()
-                elif p.val() in ("struct", "interface"):
+                elif p.val() == "struct":
+                    p.next()
+                    pkg.structs[tname] = p.struct_fields()
+                elif p.val() == "interface":
                     p.next()
                     p.skip_balanced()
                 else:
@@ -426,20 +621,7 @@ class Interp:
                     p.expect(")")
                 fname = p.next()[1]
                 p.expect("(")
-                params, pending = [], []
-                while not p.accept(")"):
-                    nm = p.next()[1]
-                    if p.val() in (",", ")"):
-                        pending.append(nm)
-                        p.accept(",")
-                        continue
-                    t = p.parse_type()
-                    for q in pending + [nm]:
-                        params.append((q, t))
-                    pending = []
-                    p.accept(",")
-                for q in pending:  # unnamed params: types only
-                    params.append((None, q))
+                params = p.params()
                 while p.val() != "{":  # results
                     if p.val() == "(":
                         p.skip_balanced()
@@ -489,27 +671,55 @@ class Interp:
     def method(self, pkg_name, recv, mname, *args):
         return self._invoke(self.pkgs[pkg_name].methods[(recv.t, mname)], recv, list(args))
 
+    def _bind(self, params, args, scope, pkg):
+        """Parameters into scope; a final ...T parameter takes the remaining
+        arguments as a slice."""
+        for k, (nm, t) in enumerate(params):
+            if t.startswith("..."):
+                v = GoList(args[k:], "[]" + t[3:])
+            else:
+                v = self._convert(args[k], t, pkg) if k < len(args) else self._zero(t, pkg)
+            if nm is not None and nm != "_":
+                scope[nm] = v
+
+    def _run(self, body, env, pkg, key):
+        sink = {} if key in self.watch else None
+        try:
+            self._exec_block(body, env, pkg, sink)
+        except Return as r:
+            return r.vals[0] if len(r.vals) == 1 else tuple(r.vals)
+        finally:
+            if sink is not None:
+                self.frames[key] = sink
+        return None
+
     def _invoke(self, fn, recv, args):
         if fn.body is None:
             fn.body = Parser(fn.toks, fn.body_at).block()
         env = [{}]
         if fn.recv:
             env[0][fn.recv[0]] = recv
-        for (nm, t), a in zip(fn.params, args):
-            if nm is not None:
-                env[0][nm] = self._convert(a, t, fn.pkg)
+        self._bind(fn.params, args, env[0], fn.pkg)
+        self._fn_stack.append(fn.name)
         try:
-            self._exec_block(fn.body, env, fn.pkg)
-        except Return as r:
-            return r.vals[0] if len(r.vals) == 1 else tuple(r.vals)
-        return None
+            return self._run(fn.body, env, fn.pkg, (fn.pkg.name, fn.name))
+        finally:
+            self._fn_stack.pop()
 
-    def _exec_block(self, stmts, env, pkg):
+    def _invoke_closure(self, c, args):
+        env = c.env + [{}]
+        self._bind(c.params, args, env[-1], c.pkg)
+        return self._run(c.body, env, c.pkg, (c.pkg.name, c.owner + ".func"))
+
+    def _exec_block(self, stmts, env, pkg, sink=None):
         env.append({})
         try:
             for s in stmts:
                 self._exec(s, env, pkg)
         finally:
+            if sink is not None:
+                for scope in env[1:]:
+                    sink.update(scope)
             env.pop()
 
     def _lookup(self, name, env):
@@ -562,6 +772,24 @@ class Interp:
                         self._exec(post, env, pkg)
             finally:
                 env.pop()
+        elif k == "range":
+            _, keys, define, x, body = s
+            seq = self._eval(x, env, pkg)
+            n = seq.len if isinstance(seq, (Slice, GoList)) else len(seq.b)
+            for i in range(n):
+                vals = [Int(i, "int"), seq.get(i) if not isinstance(seq, Str) else Int(seq.b[i], "uint8")]
+                env.append({})
+                try:
+                    for key, v in zip(keys, vals):
+                        if key[0] == "name" and key[1] == "_":
+                            continue
+                        if define:
+                            env[-1][key[1]] = v
+                        else:
+                            self._store(key, v, env, pkg)
+                    self._exec_block(body, env, pkg)
+                finally:
+                    env.pop()
         elif k == "block":
             self._exec_block(s[1], env, pkg)
         else:
@@ -573,7 +801,16 @@ class Interp:
             old = scope[target[1]]
             scope[target[1]] = self._convert(v, old.t, pkg) if isinstance(old, Int) else v
         elif target[0] == "index":
-            self._eval(target[1], env, pkg).set(self._int(self._eval(target[2], env, pkg)), v.v)
+            base = self._eval(target[1], env, pkg)
+            base.set(self._int(self._eval(target[2], env, pkg)), v if isinstance(base, GoList) else v.v)
+        elif target[0] == "sel":
+            st = self._eval(target[1], env, pkg)
+            if not isinstance(st, Struct):
+                raise NotImplementedError(target)
+            old = st.f[target[2]]
+            st.f[target[2]] = self._convert(v, old.t, st.pkg) if isinstance(old, Int) else v
+        elif target[0] == "un" and target[1] == "*":
+            self._store(target[2], v, env, pkg)
         else:
             raise NotImplementedError(target)
 
@@ -581,8 +818,38 @@ class Interp:
     def _int(x):
         return x.v if isinstance(x, Int) else int(x)
 
+    def _struct_def(self, t, pkg):
+        """(fields, package) of struct type t (plain or pkg-qualified), or None."""
+        if "." in t:
+            q, n = t.split(".", 1)
+            other = self.pkgs.get(pkg.imports.get(q, q))
+            return (other.structs[n], other, n) if other and n in other.structs else None
+        for p in [pkg] + list(self.pkgs.values()):
+            if t in p.structs:
+                return p.structs[t], p, t
+        return None
+
     def _zero(self, t, pkg):
-        return Int(0, t) if t in WIDTH else None
+        if t is None or t.startswith("*") or t in ("map", "chan", "func"):
+            return None
+        if t == "bool":
+            return False
+        sd = self._struct_def(t, pkg)
+        if sd is not None:
+            fields, spkg, name = sd
+            return Struct(name, spkg, {f: self._zero(ft, spkg) for f, ft in fields})
+        rt = self._resolve_type(t, pkg)
+        u = self._underlying(rt, pkg)
+        if u in WIDTH:
+            return Int(0, u)
+        if u == "string":
+            return Str(b"", rt)
+        if u.startswith("[") and u[1] != "]":  # [N]T
+            n = u[1:u.index("]")]
+            if n.isdigit() and u.endswith("byte"):
+                return Slice(bytearray(int(n)), 0, int(n), int(n), rt)
+            return None
+        return None  # nil: slices, pointers, interfaces, maps, channels, funcs
 
     def _resolve_type(self, t, pkg):
         if t in WIDTH or t in ("string", "bool") or t.startswith("[]"):
@@ -623,6 +890,10 @@ class Interp:
     def _binop(self, op, a, b):
         if op in ("&&", "||"):
             raise NotImplementedError
+        if a is None or b is None:  # x == nil / x != nil (nil slices, pointers, errors)
+            if op not in ("==", "!="):
+                raise GoPanic("invalid memory address or nil pointer dereference")
+            return (a is b) if op == "==" else (a is not b)
         if isinstance(a, Int) and isinstance(b, Int):
             t = a.t if a.t != "untyped" else b.t
             if op in ("<<", ">>"):
@@ -672,6 +943,8 @@ class Interp:
                 return scope[n]
             if n in ("true", "false"):
                 return n == "true"
+            if n == "nil":
+                return None
             if n in pkg.consts:
                 return self._const(pkg, n)
             raise NameError(n)
@@ -684,6 +957,8 @@ class Interp:
             return self._binop(op, self._eval(e[2], env, pkg), self._eval(e[3], env, pkg))
         if k == "un":
             x = self._eval(e[2], env, pkg)
+            if e[1] in ("&", "*"):  # pointers: the value itself (shared, see module doc)
+                return x
             if e[1] == "!":
                 return not x
             if e[1] == "-":
@@ -701,11 +976,26 @@ class Interp:
             hi = None if e[3] is None else self._int(self._eval(e[3], env, pkg))
             if isinstance(s, Str):
                 hi = len(s.b) if hi is None else hi
+                if not 0 <= lo <= hi <= len(s.b):
+                    raise GoPanic(f"slice bounds out of range [{lo}:{hi}] with length {len(s.b)}")
                 return Str(s.b[lo:hi], s.t)
-            return s.sub(lo, hi)
+            r = s.sub(lo, hi)
+            if e[4] is not None:  # 3-index slice: the capacity is cut too
+                mx = self._int(self._eval(e[4], env, pkg))
+                if not r.len + lo <= mx <= s.cap:
+                    raise GoPanic(f"slice bounds out of range [::{mx}] with capacity {s.cap}")
+                r.cap = mx - lo
+            return r
         if k == "slicelit":
             vals = [self._eval(x, env, pkg) for x in e[2]]
-            return from_bytes(bytes(v.v & 0xFF for v in vals))
+            if e[1] in ("[]byte", "[]uint8"):
+                return from_bytes(bytes(v.v & 0xFF for v in vals))
+            return GoList(vals, e[1])
+        if k == "funclit":
+            owner = self._fn_stack[-1] if self._fn_stack else "?"
+            return Closure(e[1], e[2], list(env), pkg, owner)
+        if k == "complit":
+            return self._complit(e, env, pkg)
         if k == "call":
             return self._call(e, env, pkg)
         if k == "sel":
@@ -714,7 +1004,32 @@ class Interp:
                 other = self.pkgs.get(pkg.imports[base[1]])
                 if other is not None and e[2] in other.consts:
                     return self._const(other, e[2])
-            raise NotImplementedError(e)
+                raise NameError(f"{base[1]}.{e[2]}")
+            st = self._eval(base, env, pkg)
+            if isinstance(st, Struct):
+                return st.f[e[2]]
+            return getattr(st, e[2])  # a Python stub's attribute
+        raise NotImplementedError(k)
+
+    def _complit(self, e, env, pkg):
+        """T{...} / pkg.T{...}: a struct (keyed or positional fields) or a named slice."""
+        tx, items = e[1], e[2]
+        t = tx[1] if tx[0] == "name" else f"{tx[1][1]}.{tx[2]}"
+        sd = self._struct_def(t, pkg)
+        if sd is None:
+            rt = self._resolve_type(t, pkg)
+            u = self._underlying(rt, pkg)
+            vals = [self._eval(x, env, pkg) for _, x in items]
+            if u in ("[]byte", "[]uint8"):
+                return from_bytes(bytes(v.v & 0xFF for v in vals), rt)
+            return GoList(vals, rt)
+        fields, spkg, name = sd
+        st = self._zero(t, pkg)
+        types = dict(fields)
+        for k, (key, x) in enumerate(items):
+            f = key if key is not None else fields[k][0]
+            st.f[f] = self._convert(self._eval(x, env, pkg), types[f], spkg)
+        return st
         raise NotImplementedError(k)
 
     def _const(self, pkg, n):
@@ -730,7 +1045,11 @@ class Interp:
             if self._lookup(n, env) is None:
                 if n == "len":
                     x = self._eval(args[0], env, pkg)
-                    return Int(x.len if isinstance(x, Slice) else len(x.b), "int")
+                    if x is None:  # a nil slice
+                        return Int(0, "int")
+                    return Int(x.len if isinstance(x, (Slice, GoList)) else len(x.b), "int")
+                if n == "cap":
+                    return Int(self._eval(args[0], env, pkg).cap, "int")
                 if n == "make":
                     t = args[0][1]
                     size = self._int(self._eval(args[1], env, pkg))
@@ -745,6 +1064,12 @@ class Interp:
                     return self._convert(self._eval(args[0], env, pkg), n, pkg)
                 if n in pkg.funcs:
                     return self._invoke(pkg.funcs[n], None, [self._eval(a, env, pkg) for a in args])
+            else:
+                f = self._lookup(n, env)[n]
+                if isinstance(f, Closure):
+                    return self._invoke_closure(f, [self._eval(a, env, pkg) for a in args])
+                if callable(f):
+                    return f(*[self._eval(a, env, pkg) for a in args])
             raise NameError(n)
         if fexpr[0] == "sel":
             base, name = fexpr[1], fexpr[2]
@@ -768,18 +1093,27 @@ class Interp:
                     return None
                 raise NotImplementedError(name)
             if base[0] == "name" and self._lookup(base[1], env) is None and base[1] in pkg.imports:
-                other = self.pkgs[pkg.imports[base[1]]]
                 vals = [self._eval(a, env, pkg) for a in args]
+                stub = self.stubs.get(f"{pkg.imports[base[1]]}.{name}")
+                if stub is not None:
+                    return stub(*vals)
+                other = self.pkgs[pkg.imports[base[1]]]
                 if name in other.funcs:
                     return self._invoke(other.funcs[name], None, vals)
                 if name in other.types:
                     return self._convert(vals[0], name, other)
                 raise NameError(f"{base[1]}.{name}")
             recv = self._eval(base, env, pkg)
-            for p in [pkg] + list(self.pkgs.values()):
+            vals = [self._eval(a, env, pkg) for a in args]
+            if not isinstance(recv, (Int, Slice, Str, Struct, GoList)):  # a Python stub
+                return getattr(recv, name)(*vals)
+            if isinstance(recv, Struct) and isinstance(recv.f.get(name), Closure):  # a func-typed field
+                return self._invoke_closure(recv.f[name], vals)
+            home = [recv.pkg] if isinstance(recv, Struct) else []
+            for p in home + [pkg] + list(self.pkgs.values()):
                 fn = p.methods.get((recv.t, name))
                 if fn is not None:
-                    return self._invoke(fn, recv, [self._eval(a, env, pkg) for a in args])
+                    return self._invoke(fn, recv, vals)
             raise NameError(f"method {recv.t}.{name}")
         raise NotImplementedError(fexpr)
 
@@ -789,4 +1123,22 @@ def load_reference(root="/root/reference"):
     it = Interp(root)
     it.load("checksum", ["checksum.go"])
     it.load("header", ["ipv4.go", "tcp.go", "udp.go"])
+    return it
+
+
+def load_path(root="/root/reference"):
+    """Everything from the senders to the checker: the packages above, the buffers and
+    route the senders use, the senders themselves (sendUDP, sendTCP /
+    sendTCPWithOptions, sendICMPv4, ipv4 endpoint.WritePacket) and checker.go. Only the
+    files that hold them are read; bodies are parsed when first run."""
+    it = Interp(root)
+    it.load("checksum", ["checksum.go"])
+    it.load("seqnum", ["seqnum.go"])
+    it.load("buffer", ["view.go", "prependable.go"])
+    it.load("types", ["types.go", "route.go", "transport.go", "network.go"])
+    it.load("header", ["ipv4.go", "tcp.go", "udp.go", "icmpv4.go"])
+    it.load("transport/udp", ["endpoint.go", "protocol.go"])
+    it.load("transport/tcp", ["connect.go", "protocol.go"])
+    it.load("network/ipv4", ["ipv4.go", "icmp.go"])
+    it.load("checker", ["checker.go"])
     return it

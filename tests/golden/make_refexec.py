@@ -4,20 +4,36 @@ reference's own Go source for the checksum path.
 
 The reference is Go and this image has no Go toolchain. tests/golden/goexec.py is a
 minimal interpreter for the Go subset these files use; it loads, at generation time
-only, /root/reference/checksum/checksum.go and /root/reference/header/{ipv4,tcp,udp}.go
-(nothing is copied into this repo) and runs their functions and methods:
+only, the reference's files under /root/reference (nothing is copied into this repo)
+and runs them:
 
-* checksum.Checksum, checksum.ChecksumCombine, checksum.PseudoHeaderChecksum;
-* header.IPv4.{CalculateChecksum, IsValid, HeaderLength, TotalLength, Protocol,
-  Payload, SourceAddress...}, header.TCP.{CalculateChecksum, DataOffset},
-  header.UDP.CalculateChecksum.
+* checksum.Checksum, ChecksumCombine, PseudoHeaderChecksum (checksum/checksum.go);
+* the senders, end to end: sendUDP (transport/udp/endpoint.go:164-187), sendTCP and
+  sendTCPWithOptions (transport/tcp/connect.go:556-586, :288-322), sendICMPv4
+  (network/ipv4/icmp.go:36-45), each through types.Route (types/route.go) into the
+  ipv4 endpoint's WritePacket (network/ipv4/ipv4.go:80-97), with the UDP / TCP /
+  IPv4 Encode, CalculateChecksum and SetChecksum methods of header/ and the
+  Prependable of buffer/prependable.go. A stub link endpoint takes what WritePacket
+  hands it (hdr.UsedBytes() + payload, as tundev's writev does,
+  link/tundev/tundev.go:56-58,171-196): the datagram the reference would put on the
+  wire. Its stored checksum fields are the expected TX values;
+* the checker: checker.IPv4 (checker/checker.go:25-40) and the function checker.TCP
+  returns (:71-99), with a stub *testing.T whose Fatalf ends the check as
+  runtime.Goexit does. The sum each computes (`xsum`) is read from the interpreter's
+  frame of that function, so the verify values are the checker's own.
 
-The few lines that glue them together per batch mode are restated below from the
-reference call sites they follow (file:line in each helper). Expected values in the
-fixture therefore come from the reference's code, not from oracle/. The generator
-asserts that oracle/ (C and Python) agrees on every vector; tests/test_oracle.py
-re-checks that on every CPU run, and tests/test_gpu_parity.py checks the HIP path
-against the same vectors.
+Restated (not executed), each marked "src": "restated" in the fixture, because no
+reference function computes them:
+* VERIFY_UDP and the UDP / ICMP parts of VERIFY_RX — the reference never verifies UDP
+  or ICMP (transport/udp/endpoint.go:191-229); this repo applies checker.TCP's formula
+  (and sendICMPv4's sum) to them;
+* IPv4 headers WritePacket never encodes (IHL other than 5) and TX_DATAGRAM's results
+  outside its contract (include/yucsum.h) — the field value is still the executed
+  IPv4.CalculateChecksum, only the `^` and the contract rule are restated;
+* RAW vectors call checksum.Checksum directly (executed; there is no glue).
+The generator asserts that oracle/ (C and Python) agrees on every vector;
+tests/test_oracle.py re-checks that on every CPU run, and tests/test_gpu_parity.py
+checks the HIP path against the same vectors.
 
 Run from the repo root: python tests/golden/make_refexec.py
 """
@@ -40,13 +56,44 @@ from oracle import oracle as O  # noqa: E402
 
 REF = "/root/reference"
 U16 = lambda v: G.Int(v, "uint16")  # noqa: E731
+U32 = lambda v: G.Int(v, "uint32")  # noqa: E731
+
+
+class TestingT:
+    """Stub *testing.T: Fatalf records the message and its arguments and ends the
+    check (runtime.Goexit in Go; an exception here)."""
+
+    def __init__(self):
+        self.failed = []
+
+    def Fatalf(self, fmt, *args):  # noqa: N802 (Go method name)
+        self.failed.append((fmt.b.decode(), [a.v if isinstance(a, G.Int) else a for a in args]))
+        raise G.GoFatal(fmt.b.decode())
+
+
+class LinkStub:
+    """The link endpoint under the ipv4 endpoint: what tundev's WritePacket would
+    write (hdr.UsedBytes() then the payload, link/tundev/tundev.go:56-58)."""
+
+    def __init__(self, it):
+        self.it, self.sent = it, []
+
+    def MaxHeaderLength(self):  # noqa: N802
+        return G.Int(0, "uint16")
+
+    def WritePacket(self, r, hdr, payload, protocol):  # noqa: N802
+        used = self.it.method("buffer", hdr, "UsedBytes")
+        self.sent.append(used.bytes() + (payload.bytes() if payload is not None else b""))
+        return None
 
 
 class Ref:
     """The reference's functions, executed by goexec."""
 
     def __init__(self):
-        self.it = G.load_reference(REF)
+        self.it = G.load_path(REF)
+        self.it.watch |= {("checker", "IPv4"), ("checker", "TCP.func")}
+        self.link = LinkStub(self.it)
 
     def checksum(self, b: bytes, initial: int) -> int:
         return self.it.call("checksum", "Checksum", G.from_bytes(b), U16(initial)).v
@@ -61,80 +108,85 @@ class Ref:
     def m(self, typ: str, b: bytes, name: str, *args):
         return self.it.method("header", G.from_bytes(b, typ), name, *args)
 
-    # --- TX compositions (field value the sender stores) --------------------------
-    def tcp_field(self, seg: bytes, src: bytes, dst: bytes) -> int:
-        """transport/tcp/connect.go:576-583 (sendTCP) and :310-317 (with options):
-        the header is Encode()d with checksum 0 (header/tcp.go:176-186), the data
-        follows DataOffset(); route.PseudoHeaderChecksum(6) = checksum.
-        PseudoHeaderChecksum(6, local, remote) (types/route.go:90-92)."""
-        hdr = bytearray(seg)
-        hdr[16:18] = b"\x00\x00"
-        doff = self.m("TCP", bytes(hdr), "DataOffset").v
-        data = bytes(seg[doff:])
-        xsum = self.pseudo(6, src, dst)
-        length = len(seg) & 0xFFFF
-        xsum = self.checksum(data, xsum)
-        r = self.m("TCP", bytes(hdr), "CalculateChecksum", U16(xsum), U16(length)).v
-        return ~r & 0xFFFF
+    # --- the senders, executed end to end -----------------------------------------
+    def route(self, src: bytes, dst: bytes):
+        """A types.Route from src to dst over an ipv4 endpoint whose address is src
+        (network/ipv4/ipv4.go:31-38 fields; types/route.go:14-36)."""
+        ep = self.it._zero("endpoint", self.it.pkgs["ipv4"])
+        ep.f["address"] = G.from_bytes(src, "address")
+        ep.f["linkEp"] = self.link
+        r = self.it._zero("Route", self.it.pkgs["types"])
+        r.f["LocalAddress"], r.f["RemoteAddress"] = G.Str(src, "Address"), G.Str(dst, "Address")
+        r.f["NetEp"] = ep
+        return r
 
-    def udp_field(self, dgram: bytes, src: bytes, dst: bytes) -> int:
-        """transport/udp/endpoint.go:171-184 (sendUDP): Encode() leaves the checksum
-        field 0 (header/udp.go:78-83), data follows the 8-byte header."""
-        hdr = bytearray(dgram)
-        hdr[6:8] = b"\x00\x00"
-        xsum = self.pseudo(17, src, dst)
-        xsum = self.checksum(bytes(dgram[8:]), xsum)
-        r = self.m("UDP", bytes(hdr), "CalculateChecksum", U16(xsum), U16(len(dgram) & 0xFFFF)).v
-        return ~r & 0xFFFF
+    def _sent(self):
+        return self.link.sent.pop()
 
+    @staticmethod
+    def _view(data):
+        return None if data is None else G.from_bytes(data, "View")
+
+    def send_udp(self, src, dst, data, lport, rport) -> bytes:
+        """transport/udp/endpoint.go:164-187 -> network/ipv4/ipv4.go:80-97."""
+        self.it.call("udp", "sendUDP", self.route(src, dst), self._view(data), U16(lport), U16(rport))
+        return self._sent()
+
+    def send_tcp(self, src, dst, data, lport, rport, flags, seq, ack, wnd, opts=None) -> bytes:
+        """transport/tcp/connect.go:556-586 (sendTCP) or, with options, :288-322
+        (sendTCPWithOptions, as sendSynTCP calls it)."""
+        tid = self.it._zero("TransportEndpointId", self.it.pkgs["types"])
+        tid.f["LocalPort"], tid.f["RemotePort"] = U16(lport), U16(rport)
+        args = [self.route(src, dst), tid, self._view(data), G.Int(flags, "uint8"), U32(seq), U32(ack), U32(wnd)]
+        if opts is None:
+            self.it.call("tcp", "sendTCP", *args)
+        else:
+            self.it.call("tcp", "sendTCPWithOptions", *args, G.from_bytes(opts))
+        return self._sent()
+
+    def send_icmp(self, src, dst, typ, code, data) -> bytes:
+        """network/ipv4/icmp.go:36-45."""
+        self.it.call("ipv4", "sendICMPv4", self.route(src, dst), G.Int(typ, "uint8"), G.Int(code, "uint8"),
+                     self._view(data))
+        return self._sent()
+
+    # --- the checker, executed ----------------------------------------------------
+    def checker_ipv4(self, pkt: bytes):
+        """checker.IPv4(t, b) (checker/checker.go:25-40): (passed, xsum it computed)."""
+        t = TestingT()
+        self.it.frames.pop(("checker", "IPv4"), None)
+        try:
+            self.it.call("checker", "IPv4", t, G.from_bytes(pkt))
+        except G.GoFatal:
+            pass
+        x = self.it.frames.get(("checker", "IPv4"), {}).get("xsum")
+        return not t.failed, (None if x is None else x.v)
+
+    def checker_tcp(self, pkt: bytes):
+        """The function checker.TCP() returns (checker/checker.go:71-99), run on the
+        datagram's IPv4 header as checker.IPv4 would pass it: (passed, xsum)."""
+        t = TestingT()
+        f = self.it.call("checker", "TCP")
+        net = G.GoList([G.from_bytes(pkt, "IPv4")], "[]Network")
+        self.it.frames.pop(("checker", "TCP.func"), None)
+        try:
+            self.it._invoke_closure(f, [t, net])
+        except G.GoFatal:
+            pass
+        x = self.it.frames.get(("checker", "TCP.func"), {}).get("xsum")
+        return not t.failed, (None if x is None else x.v)
+
+    # --- restated glue (no reference function computes these) ---------------------
     def ipv4_field(self, pkt: bytes) -> int:
-        """network/ipv4/ipv4.go:85-94: Encode() with checksum 0 (header/ipv4.go:146-157),
-        then SetChecksum(^CalculateChecksum())."""
+        """network/ipv4/ipv4.go:85-94 for a header WritePacket never encodes (any IHL):
+        ^IPv4.CalculateChecksum() (executed) with the field 0."""
         b = bytearray(pkt)
         b[10:12] = b"\x00\x00"
         return ~self.m("IPv4", bytes(b), "CalculateChecksum").v & 0xFFFF
 
-    def icmp_field(self, msg: bytes) -> int:
-        """network/ipv4/icmp.go:36-45: ^Checksum(icmpv4 header (field 0), Checksum(data, 0))."""
-        hdr = bytearray(msg[:4])
-        hdr[2:4] = b"\x00\x00"
-        return ~self.checksum(bytes(hdr), self.checksum(bytes(msg[4:]), 0)) & 0xFFFF
-
-    def tx_datagram(self, pkt: bytes) -> list:
-        """YU_MODE_TX_DATAGRAM (include/yucsum.h): a whole outgoing datagram's two
-        fields — ipv4.WritePacket's header field (network/ipv4/ipv4.go:85-94) and the
-        transport field its sender stored before (sendUDP / sendTCP / sendICMPv4),
-        with the route addresses = the header's SourceAddress / DestinationAddress
-        (ipv4.go:84-92 encodes them from the same route) over Payload()."""
-        if len(pkt) < 20:
-            return [0, 0]
-        hl = self.m("IPv4", pkt, "HeaderLength").v
-        tl = self.m("IPv4", pkt, "TotalLength").v
-        if hl < 20 or not self.m("IPv4", pkt, "IsValid", G.Int(len(pkt), "int")):
-            return [0, 0]
-        ip = self.ipv4_field(pkt)
-        proto = self.m("IPv4", pkt, "Protocol").v
-        seg = self.m("IPv4", pkt, "Payload").bytes()
-        assert len(seg) == tl - hl
-        # SourceAddress() / DestinationAddress() are b[12:16] / b[16:20]
-        # (header/ipv4.go:111-118; their types.Address is outside goexec's packages)
-        src, dst = pkt[12:16], pkt[16:20]
-        l4 = 0
-        if proto == 17 and len(seg) >= 8:
-            l4 = self.udp_field(seg, src, dst)
-        elif proto == 6 and len(seg) >= 20:
-            l4 = self.tcp_field(seg, src, dst)
-        elif proto == 1 and len(seg) >= 4:
-            l4 = self.icmp_field(seg)
-        return [ip, l4]
-
-    # --- receive-side verification (checker semantics) ------------------------------
-    def verify_ipv4(self, pkt: bytes) -> int:
-        """checker/checker.go:32-35: the sum over b[:HeaderLength()] incl. the field."""
-        return self.m("IPv4", pkt, "CalculateChecksum").v
-
     def verify_l4(self, seg: bytes, src: bytes, dst: bytes, proto: int) -> int:
-        """checker/checker.go:80-92 (checker.TCP), the same formula for UDP."""
+        """checker.TCP's formula (checker/checker.go:84-88) for a UDP datagram: the
+        reference never verifies UDP."""
         l = len(seg) & 0xFFFF
         x = self.checksum(src, 0)
         x = self.checksum(dst, x)
@@ -142,29 +194,60 @@ class Ref:
         x = self.checksum(bytes([l >> 8, l & 0xFF]), x)
         return self.checksum(seg, x)
 
-    def rx_flags(self, pkt: bytes) -> int:
-        """YU_MODE_VERIFY_RX (include/yucsum.h): IPv4.IsValid (header/ipv4.go:126-138),
-        checker.IPv4's header test and checker.TCP's transport test over
-        Payload() = b[HeaderLength():][:PayloadLength()] (header/ipv4.go:181-189) with
-        the addresses and protocol read from the packet; ICMP without the pseudo
-        header (network/ipv4/icmp.go:36-45)."""
+    def rx_flags(self, pkt: bytes):
+        """YU_MODE_VERIFY_RX (include/yucsum.h): IPv4.IsValid (header/ipv4.go:126-138,
+        executed), checker.IPv4's header sum and, for TCP, checker.TCP's transport sum
+        (both executed); UDP and ICMP restated (the reference verifies neither).
+        Returns (flags, "exec" | "restated")."""
         if not self.m("IPv4", pkt, "IsValid", G.Int(len(pkt), "int")):
-            return 8
-        r = 0
-        s = self.verify_ipv4(pkt)
-        if s in (0, 0xFFFF):
-            r |= 1
+            return 8, "exec"
+        _, s = self.checker_ipv4(pkt)
+        r = 1 if s in (0, 0xFFFF) else 0
         proto = self.m("IPv4", pkt, "Protocol").v
-        if proto in (1, 6, 17):
+        src = "exec"
+        if proto == 6:
             r |= 2
+            _, s = self.checker_tcp(pkt)
+            r |= 4 if s in (0, 0xFFFF) else 0
+        elif proto in (1, 17):
+            r |= 2
+            src = "restated"
             payload = self.m("IPv4", pkt, "Payload").bytes()
-            if proto == 1:
-                s = self.checksum(payload, 0)
-            else:
-                s = self.verify_l4(payload, pkt[12:16], pkt[16:20], proto)
-            if s in (0, 0xFFFF):
-                r |= 4
-        return r
+            s = self.checksum(payload, 0) if proto == 1 else self.verify_l4(payload, pkt[12:16], pkt[16:20], 17)
+            r |= 4 if s in (0, 0xFFFF) else 0
+        return r, src
+
+    def tx_contract(self, pkt: bytes) -> list:
+        """TX_DATAGRAM's rule for datagrams no sender built (include/yucsum.h): {0, 0}
+        outside 20 <= HeaderLength() <= TotalLength() <= len; the transport value 0 for
+        another protocol or a segment shorter than its header; otherwise the
+        executed header methods and the sender formulas on the segment."""
+        if len(pkt) < 20:
+            return [0, 0]
+        hl = self.m("IPv4", pkt, "HeaderLength").v
+        if hl < 20 or not self.m("IPv4", pkt, "IsValid", G.Int(len(pkt), "int")):
+            return [0, 0]
+        ip = self.ipv4_field(pkt)
+        proto = self.m("IPv4", pkt, "Protocol").v
+        seg = self.m("IPv4", pkt, "Payload").bytes()
+        src, dst = pkt[12:16], pkt[16:20]
+        l4 = 0
+        if proto == 17 and len(seg) >= 8:
+            u = bytearray(seg)
+            u[6:8] = b"\x00\x00"
+            x = self.checksum(bytes(seg[8:]), self.pseudo(17, src, dst))
+            l4 = ~self.m("UDP", bytes(u), "CalculateChecksum", U16(x), U16(len(seg) & 0xFFFF)).v & 0xFFFF
+        elif proto == 6 and len(seg) >= 20:
+            t = bytearray(seg)
+            t[16:18] = b"\x00\x00"
+            doff = self.m("TCP", bytes(t), "DataOffset").v
+            x = self.checksum(bytes(seg[doff:]), self.pseudo(6, src, dst))
+            l4 = ~self.m("TCP", bytes(t), "CalculateChecksum", U16(x), U16(len(seg) & 0xFFFF)).v & 0xFFFF
+        elif proto == 1 and len(seg) >= 4:
+            h = bytearray(seg[:4])
+            h[2:4] = b"\x00\x00"
+            l4 = ~self.checksum(bytes(h), self.checksum(bytes(seg[4:]), 0)) & 0xFFFF
+        return [ip, l4]
 
 
 def vec_bytes(v):
@@ -228,55 +311,117 @@ def main() -> None:
             pseudo.append({"proto": proto, "src": src.hex(), "dst": dst.hex(), "want": want})
     out["pseudo"] = pseudo
 
-    # batch-mode vectors: packet bytes (checksum fields left random: TX modes take
-    # them as 0), addresses {src, dst}, expected value from the reference
+    # batch-mode vectors: packet bytes (TX modes: the checksum fields overwritten with
+    # garbage, which the modes take as 0), addresses {src, dst}, the expected value,
+    # and where it came from ("exec": the reference's sender / checker run end to end;
+    # "restated": see the module doc)
     modes = {}
 
-    def add(mode, pkt, addrs, want):
-        modes.setdefault(str(mode), []).append({"hex": pkt.hex(), "addrs": addrs.hex(), "want": want})
+    def add(mode, pkt, addrs, want, src="exec"):
+        modes.setdefault(str(mode), []).append({"hex": pkt.hex(), "addrs": addrs.hex(), "want": want,
+                                                "src": src})
 
-    for _ in range(60):
-        n = rng.choice([20, 21, 24, 40, 41, 60, 61, 200, 1460, 1500, rng.randint(20, 1600)])
-        doff = 4 * rng.randint(5, min(15, n // 4))
-        seg = bytearray(rnd(rng, n))
-        seg[12] = (doff // 4) << 4 | (seg[12] & 0x0F)
+    def garble(b, at):
+        b = bytearray(b)
+        b[at:at + 2] = rnd(rng, 2)
+        return bytes(b)
+
+    def flip(b, lo=0):
+        b = bytearray(b)
+        i = rng.randrange(lo, len(b)) if len(b) > lo else None
+        if i is not None:
+            b[i] ^= 1 << rng.randrange(8)
+        return bytes(b)
+
+    be16 = lambda b, at: b[at] << 8 | b[at + 1]  # noqa: E731
+    sent = []  # (datagram, proto) the senders put on the wire
+
+    # TCP: sendTCP (DataOffset 20) and sendTCPWithOptions (options of 4..40 bytes, as
+    # sendSynTCP passes them) with random ports, sequence numbers, flags and windows
+    # (some above 0xffff: the clamp at connect.go:559-561), payloads of 0..1600 bytes
+    for k in range(70):
         a = rnd(rng, 8)
-        add(O.MODE_TCP, bytes(seg), a, ref.tcp_field(bytes(seg), a[:4], a[4:]))
-        add(O.MODE_VERIFY_TCP, bytes(seg), a, ref.verify_l4(bytes(seg), a[:4], a[4:], 6))
-    for _ in range(60):
-        n = rng.choice([8, 9, 10, 72, 73, 1472, rng.randint(8, 1600)])
-        d = rnd(rng, n)
+        n = rng.choice([0, 1, 2, 3, 40, 41, 1460, 1480, rng.randint(0, 1600)])
+        data = rnd(rng, n) if n or k % 2 else None
+        opts = None if k % 3 == 0 else rnd(rng, 4 * rng.randint(0, 10))
+        dg = ref.send_tcp(a[:4], a[4:], data, rng.getrandbits(16), rng.getrandbits(16), rng.getrandbits(8),
+                          rng.getrandbits(32), rng.getrandbits(32), rng.getrandbits(17), opts)
+        seg = dg[20:]
+        add(O.MODE_TCP, garble(seg, 16), a, be16(seg, 16))
+        sent.append((dg, 6))
+        # checker.TCP over the segment as sent, or with a bit flipped: its own xsum
+        sg = seg if k % 2 else flip(seg)
+        ok, x = ref.checker_tcp(dg[:20] + sg)
+        assert ok == (x in (0, 0xFFFF))
+        add(O.MODE_VERIFY_TCP, sg, a, x)
+    # UDP: sendUDP, payloads of 0..1600 bytes (nil and empty views included)
+    for k in range(70):
         a = rnd(rng, 8)
-        add(O.MODE_UDP, d, a, ref.udp_field(d, a[:4], a[4:]))
-        add(O.MODE_VERIFY_UDP, d, a, ref.verify_l4(d, a[:4], a[4:], 17))
+        n = rng.choice([0, 1, 2, 3, 64, 65, 1472, rng.randint(0, 1600)])
+        data = rnd(rng, n) if n or k % 2 else None
+        dg = ref.send_udp(a[:4], a[4:], data, rng.getrandbits(16), rng.getrandbits(16))
+        seg = dg[20:]
+        add(O.MODE_UDP, garble(seg, 6), a, be16(seg, 6))
+        sent.append((dg, 17))
+        sg = seg if k % 2 else flip(seg)
+        add(O.MODE_VERIFY_UDP, sg, a, ref.verify_l4(sg, a[:4], a[4:], 17), "restated")
+    # ICMP: sendICMPv4 (echo replies and other types), payloads of 0..1600 bytes
+    for k in range(50):
+        a = rnd(rng, 8)
+        n = rng.choice([0, 1, 4, 5, 56, 64, 65, rng.randint(0, 1600)])
+        data = rnd(rng, n) if n or k % 2 else None
+        dg = ref.send_icmp(a[:4], a[4:], rng.choice([0, 3, 8, 11, rng.getrandbits(8)]), rng.getrandbits(8), data)
+        add(O.MODE_ICMP, garble(dg[20:], 2), bytes(8), be16(dg, 22))
+        sent.append((dg, 1))
+    # IPv4 header field: every datagram a sender built (WritePacket's value), as the
+    # header alone and as the whole datagram; checker.IPv4 on them as sent and damaged
+    for i, (dg, _) in enumerate(sent):
+        if i % 2 == 0:
+            add(O.MODE_IPV4, garble(dg if i % 4 == 0 else dg[:20], 10), bytes(8), be16(dg, 10))
+        if i % 3 == 0:
+            d2 = dg if i % 2 else flip(dg[:20]) + dg[20:]
+            ok, x = ref.checker_ipv4(d2)
+            if x is not None:  # IsValid held: checker.IPv4's own sum
+                assert ok == (x in (0, 0xFFFF))
+                add(O.MODE_VERIFY_IPV4, d2, bytes(8), x)
+    # headers WritePacket never encodes: any IHL 0..15 (restated ^, executed sum)
     for _ in range(60):
         ihl = rng.randint(0, 15)
         n = max(1, 4 * ihl) + rng.choice([0, 0, 1, 3, 100])
         p = bytearray(rnd(rng, n))
         p[0] = 0x40 | ihl
-        add(O.MODE_IPV4, bytes(p), bytes(8), ref.ipv4_field(bytes(p)))
-        add(O.MODE_VERIFY_IPV4, bytes(p), bytes(8), ref.verify_ipv4(bytes(p)))
-    for _ in range(40):
-        n = rng.choice([4, 5, 8, 64, 65, rng.randint(4, 1600)])
-        d = rnd(rng, n)
-        add(O.MODE_ICMP, d, bytes(8), ref.icmp_field(d))
+        add(O.MODE_IPV4, bytes(p), bytes(8), ref.ipv4_field(bytes(p)), "restated")
+        # VERIFY_IPV4 is the sum checker.IPv4 computes (checker.go:32): the executed
+        # IPv4.CalculateChecksum, which checker.IPv4 reaches only when IsValid holds
+        add(O.MODE_VERIFY_IPV4, bytes(p), bytes(8), ref.m("IPv4", bytes(p), "CalculateChecksum").v, "exec")
     for _ in range(40):
         n = rng.choice([0, 1, 2, 3, 63, 64, 65, 1500, rng.randint(0, 1600)])
         d = rnd(rng, n)
         init = rng.getrandbits(16)
         add(O.MODE_RAW, d, init.to_bytes(2, "little") + bytes(6), ref.checksum(d, init))
-    # whole received datagrams: well-formed (the reference's senders), damaged, malformed
+    # whole outgoing datagrams (TX_DATAGRAM): as the senders built them, both fields
+    # then overwritten with garbage; the values are the fields the senders stored
+    for dg, proto in sent:
+        f = {17: 6, 6: 16, 1: 2}[proto]
+        add(O.MODE_TX_DATAGRAM, garble(garble(dg, 10), 20 + f), bytes(8), [be16(dg, 10), be16(dg, 20 + f)])
+    # whole received datagrams (VERIFY_RX): as sent, with a bit flipped in the header
+    # or the payload, and rxgen's malformed and damaged ones
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import rxgen  # tests/rxgen.py: datagrams built like the reference senders
+    for i, (dg, _) in enumerate(sent):
+        if i % 2:
+            d2 = dg if i % 3 else flip(dg, 0 if i % 5 else 20)
+            f, src = ref.rx_flags(d2)
+            add(O.MODE_VERIFY_RX, d2, bytes(8), f, src)
     nrng = np.random.default_rng(16)
     blob, offs = rxgen.rx_batch(nrng, 120, lo=0, hi=1480)
     for i in range(len(offs) - 1):
         pk = bytes(blob[int(offs[i]):int(offs[i + 1])])
-        add(O.MODE_VERIFY_RX, pk, bytes(8), ref.rx_flags(pk))
-    # whole outgoing datagrams (TX_DATAGRAM): built like the reference senders, their
-    # checksum fields then overwritten with garbage (the mode takes them as 0), plus
-    # out-of-contract ones (IHL < 5, lengths that do not fit, other protocols)
-    for i in range(120):
+        f, src = ref.rx_flags(pk)
+        add(O.MODE_VERIFY_RX, pk, bytes(8), f, src)
+    # TX_DATAGRAM outside what the senders build: rxgen datagrams (any protocol, some
+    # damaged or out of contract), under the mode's contract rule (restated)
+    for i in range(60):
         pk = bytearray(rxgen.make_packet(nrng, int(nrng.integers(0, 1480)),
                                          ihl=5 if i % 3 else None))
         hl = (pk[0] & 0xF) * 4
@@ -286,11 +431,15 @@ def main() -> None:
             pk[hl + f: hl + f + 2] = rnd(rng, 2)
         if i % 10 == 9:
             pk = rxgen.tcp_contract(rxgen.damage(nrng, pk))
-        add(O.MODE_TX_DATAGRAM, bytes(pk), bytes(8), ref.tx_datagram(bytes(pk)))
+        add(O.MODE_TX_DATAGRAM, bytes(pk), bytes(8), ref.tx_contract(bytes(pk)), "restated")
     for ihl in (0, 1, 4):  # HeaderLength() under 20: outside the contract
         pk = bytearray(rxgen.make_packet(nrng, 40, proto=17, ihl=5))
         pk[0] = 0x40 | ihl
-        add(O.MODE_TX_DATAGRAM, bytes(pk), bytes(8), ref.tx_datagram(bytes(pk)))
+        add(O.MODE_TX_DATAGRAM, bytes(pk), bytes(8), ref.tx_contract(bytes(pk)), "restated")
+    # the executed senders' fields agree with the restated contract rule where both apply
+    for dg, proto in sent:
+        f = {17: 6, 6: 16, 1: 2}[proto]
+        assert ref.tx_contract(garble(garble(dg, 10), 20 + f)) == [be16(dg, 10), be16(dg, 20 + f)]
     out["modes"] = modes
 
     # oracle agreement on every mode vector (ragged batch through the C oracle)

@@ -94,13 +94,16 @@ def test_device_count_reads_kfd_topology_without_hip(tmp_path):
     assert bench._device_count({}, nodes, dri) == 2
     assert bench._device_count({"HIP_VISIBLE_DEVICES": "1"}, nodes, dri) == 1
     assert bench._device_count({"ROCR_VISIBLE_DEVICES": "0,1", "CUDA_VISIBLE_DEVICES": "0"}, nodes, dri) == 1
-    # one HIP-level list: HIP_VISIBLE_DEVICES when non-empty, else CUDA_VISIBLE_DEVICES
-    assert bench._device_count({"HIP_VISIBLE_DEVICES": ""}, nodes, dri) == 2
-    assert bench._device_count({"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": "1"}, nodes, dri) == 1
+    # one HIP-level list: HIP_VISIBLE_DEVICES when set (empty: no device), else
+    # CUDA_VISIBLE_DEVICES; an empty ROCR_VISIBLE_DEVICES is no list (as measured on
+    # the MI355X box, tests/test_gpu_dist.py::test_launcher_device_count_matches_hip)
+    assert bench._device_count({"HIP_VISIBLE_DEVICES": ""}, nodes, dri) == 0
+    assert bench._device_count({"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": "1"}, nodes, dri) == 0
     assert bench._device_count({"HIP_VISIBLE_DEVICES": "0,1", "CUDA_VISIBLE_DEVICES": "0"}, nodes, dri) == 2
     assert bench._device_count({"HIP_VISIBLE_DEVICES": "1", "CUDA_VISIBLE_DEVICES": "7"}, nodes, dri) == 1
-    assert bench._device_count({"CUDA_VISIBLE_DEVICES": ""}, nodes, dri) == 2
-    assert bench._device_count({"ROCR_VISIBLE_DEVICES": ""}, nodes, dri) == 0
+    assert bench._device_count({"HIP_VISIBLE_DEVICES": "7", "CUDA_VISIBLE_DEVICES": "0"}, nodes, dri) == 0
+    assert bench._device_count({"CUDA_VISIBLE_DEVICES": ""}, nodes, dri) == 0
+    assert bench._device_count({"ROCR_VISIBLE_DEVICES": ""}, nodes, dri) == 2
     assert bench._device_count({"HIP_VISIBLE_DEVICES": "0,5,1"}, nodes, dri) == 1  # stops at the bad index
     assert bench._device_count({"ROCR_VISIBLE_DEVICES": "GPU-1234abcd"}, nodes, dri) == 1
     assert bench._device_count({}, str(tmp_path / "absent"), dri) == 0
