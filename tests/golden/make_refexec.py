@@ -35,7 +35,7 @@ The generator asserts that oracle/ (C and Python) agrees on every vector;
 tests/test_oracle.py re-checks that on every CPU run, and tests/test_gpu_parity.py
 checks the HIP path against the same vectors.
 
-Run from the repo root: python tests/golden/make_refexec.py
+Run from the repo root: python tests/golden/make_refexec.py [out.json]
 """
 from __future__ import annotations
 
@@ -457,7 +457,7 @@ def main() -> None:
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (mode, bad[:5], got[bad[:5]], want[bad[:5]])
 
-    path = os.path.join(HERE, "refexec.json")
+    path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(HERE, "refexec.json")
     with open(path, "w") as f:
         json.dump(out, f, separators=(",", ":"))
     print(f"wrote {path}: {sum(len(v) for v in modes.values())} mode vectors, {len(cs)} checksum, "

@@ -325,3 +325,31 @@ def test_vectorised_build_agrees(oracle_c):
     bo = np.array([0, 131073, 131073 + 140001], np.uint64)
     assert np.array_equal(oracle_c.batch(big, 0, offsets=bo, initial=0xFFFF),
                           opt.batch(big, 0, offsets=bo, initial=0xFFFF))
+
+
+def test_refexec_vectors_come_from_executed_reference(refexec):
+    """The TX and checker modes' expected values come from the reference's senders
+    and checker run end to end (tests/golden/make_refexec.py): every UDP, TCP, ICMP and
+    VERIFY_TCP vector, and most IPv4 / VERIFY_IPV4 / TX_DATAGRAM / VERIFY_RX ones; the
+    rest are marked "restated" (VERIFY_UDP, UDP / ICMP receive checks, headers and
+    datagrams no sender builds)."""
+    src = {m: [v["src"] for v in vecs] for m, vecs in refexec["modes"].items()}
+    for m in ("1", "2", "4", "6"):
+        assert set(src[m]) == {"exec"} and len(src[m]) >= 50, m
+    assert set(src["7"]) == {"restated"}
+    for m, least in (("3", 90), ("5", 100), ("8", 90), ("9", 180)):
+        assert src[m].count("exec") >= least, (m, src[m].count("exec"))
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/transport"), reason="reference source not present")
+def test_refexec_fixture_regenerates(tmp_path):
+    """Where the reference's source is present (the build container), running the
+    generator again reproduces the committed fixture byte for byte (seeded)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(REFEXEC)
+    out = tmp_path / "refexec.json"
+    r = subprocess.run([sys.executable, os.path.join(here, "make_refexec.py"), str(out)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert out.read_bytes() == open(REFEXEC, "rb").read()
