@@ -13,5 +13,9 @@ tail -15 gpurun_out/gpu_tests_$TAG.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail gpurun_out/smoke_$TAG.log; exit 1; }
 tail -1 gpurun_out/smoke_$TAG.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail gpurun_out/bench_$TAG.err; exit 1; }
-echo "bench ok; pytest rc $rc"
-exit $rc
+[ $rc -eq 0 ] || { echo "pytest rc $rc"; exit $rc; }
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${TAG}_driver.json 2> gpurun_out/bench_${TAG}_driver.err || { tail gpurun_out/bench_${TAG}_driver.err; exit 1; }
+echo bench-ok
+[ -n "${PROF_CFGS:-}" ] || exit 0
+CFGS="$PROF_CFGS" timeout -k 10 900 bash tools/profile.sh $TAG || exit 1
+echo prof-ok
