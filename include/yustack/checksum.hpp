@@ -331,6 +331,24 @@ inline void FillHostPackets(const yu_iovec *iov, const uint64_t *first_iov, uint
   if (rc) throw Error(rc, "yu_csum_fill_host_iov");
 }
 
+// Host-path staging of `device` (include/yucsum.h, "Host-path staging"): the pinned
+// and device bytes its bounded context pool holds now; at most HostContexts() x
+// YU_HOST_CONTEXT_PINNED_MAX / _DEVICE_MAX between calls.
+struct Staging {
+  uint64_t pinned, device;
+};
+inline Staging HostStaging(int device = 0) {
+  uint64_t d = 0;
+  const uint64_t p = yu_host_staging_bytes(device, &d);
+  return {p, d};
+}
+inline int HostContexts() { return yu_host_contexts(); }
+// Frees the staging of the device's idle contexts.
+inline void HostStagingTrim(int device = 0) {
+  int rc = yu_host_staging_trim(device);
+  if (rc) throw Error(rc, "yu_host_staging_trim");
+}
+
 }  // namespace batch
 }  // namespace yustack
 

@@ -16,8 +16,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "yustack/checksum.hpp"
@@ -293,6 +295,42 @@ static void test_gpu_batches() {
     for (uint64_t i = 0; i < rn; ++i)
       same &= ro_out[i] == checksum::Checksum(big.data() + ro[i], ro[i + 1] - ro[i], 0x4321);
     EXPECT(same, "host ragged pipelined (18 MB, %lu packets)", rn);
+  }
+
+  // many OS threads at once through the bounded staging pool (include/yucsum.h):
+  // direct bursts and pipelined batches from pageable memory, every result checked,
+  // the staging held afterwards within the pool's bound, then trimmed
+  {
+    const uint64_t bn = 12000, L = 1500;  // 18 MB: the sliced pipeline
+    std::vector<uint8_t> big(bn * L);
+    for (auto &b : big) b = (uint8_t)rng();
+    std::vector<uint16_t> want(bn);
+    for (uint64_t i = 0; i < bn; ++i) want[i] = checksum::Checksum(big.data() + i * L, L, 0);
+    std::atomic<int> bad{0};
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 16; ++t)
+      ts.emplace_back([&, t] {
+        std::vector<uint16_t> o(bn);
+        for (int r = 0; r < 3; ++r) {
+          const uint64_t k = t % 4 == 0 ? bn : 64;  // a quarter pipelined, the rest direct
+          try {
+            batch::HostUniform(big.data(), L, (uint32_t)L, k, batch::RAW, o.data());
+          } catch (const Error &) {
+            ++bad;
+            continue;
+          }
+          if (!std::equal(o.begin(), o.begin() + k, want.begin())) ++bad;
+        }
+      });
+    for (auto &th : ts) th.join();
+    EXPECT(bad == 0, "16 threads through the host staging pool: %d bad calls", bad.load());
+    const batch::Staging st = batch::HostStaging(0);
+    EXPECT(st.pinned > 0 && st.pinned <= (uint64_t)batch::HostContexts() * YU_HOST_CONTEXT_PINNED_MAX,
+           "pinned staging %lu within the pool bound", (unsigned long)st.pinned);
+    EXPECT(st.device <= (uint64_t)batch::HostContexts() * YU_HOST_CONTEXT_DEVICE_MAX,
+           "device staging %lu within the pool bound", (unsigned long)st.device);
+    batch::HostStagingTrim(0);
+    EXPECT(batch::HostStaging(0).pinned == 0, "trim frees the idle staging");
   }
 
   bool threw = false;

@@ -16,6 +16,13 @@ timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/ben
 [ $rc -eq 0 ] || { echo "pytest rc $rc"; exit $rc; }
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${TAG}_driver.json 2> gpurun_out/bench_${TAG}_driver.err || { tail gpurun_out/bench_${TAG}_driver.err; exit 1; }
 echo bench-ok
+if [ -n "${ASAN:-}" ]; then
+  ASAN_OPTIONS=detect_leaks=0 timeout -k 10 300 tests/cpp/build/test_checksum_asan --gpu > gpurun_out/cpp_asan_$TAG.log 2>&1 || { tail -30 gpurun_out/cpp_asan_$TAG.log; exit 1; }
+  tail -1 gpurun_out/cpp_asan_$TAG.log
+fi
+if [ -n "${FUZZ_SEED_BASE:-}" ]; then
+  bash tools/fuzz_long.sh || exit 1
+fi
 [ -n "${PROF_CFGS:-}" ] || exit 0
 CFGS="$PROF_CFGS" timeout -k 10 900 bash tools/profile.sh $TAG || exit 1
 echo prof-ok
