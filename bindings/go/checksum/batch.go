@@ -159,3 +159,21 @@ func BatchHostRagged(data []byte, offsets []uint64, mode Mode, initial []uint16,
 		C.uint64_t(n), C.int(mode), pi, 0, pa, (*C.uint16_t)(unsafe.Pointer(&out[0])), &d[0], C.int(nd)))
 }
 
+
+// HostStaging reports the pinned host and device bytes the host path's staging
+// holds for device now (include/yucsum.h yu_host_staging_bytes). Each call
+// borrows one of at most HostContexts() contexts of its device, so between
+// calls this stays within HostContexts() * YU_HOST_CONTEXT_PINNED_MAX pinned
+// bytes however many OS threads a program's goroutines have run on.
+func HostStaging(device int) (pinned, dev uint64) {
+	var d C.uint64_t
+	p := C.yu_host_staging_bytes(C.int(device), &d)
+	return uint64(p), uint64(d)
+}
+
+// HostContexts is the bound on staging contexts per device (YU_HOST_CONTEXTS,
+// default 4, read once from the environment).
+func HostContexts() int { return int(C.yu_host_contexts()) }
+
+// HostStagingTrim frees the staging of the device's idle contexts.
+func HostStagingTrim(device int) error { return status(C.yu_host_staging_trim(C.int(device))) }
