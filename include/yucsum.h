@@ -68,8 +68,9 @@ extern "C" {
 /*                                                                      */
 /*  [mode]          mode is not 0 .. YU_MODE_COUNT-1 (every call).       */
 /*  [out]           out == NULL in a yu_csum_batch_* call, or h_out ==   */
-/*                  NULL in a yu_csum_batch_host_* call (the fill calls  */
-/*                  take NULL: no result array).                         */
+/*                  NULL in a yu_csum_batch_host_* call, with n > 0 (the */
+/*                  fill calls take NULL: no result array; an empty     */
+/*                  batch, n == 0, is a no-op returning YU_OK).          */
 /*  [fill-mode]     a fill call (yu_csum_fill_*) with a mode that has no */
 /*                  field to write: RAW, VERIFY_* (or no mode at all).   */
 /*  [side-align]    device calls: initial_arr not 2-byte aligned, addrs  */

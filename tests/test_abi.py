@@ -339,6 +339,15 @@ def test_each_documented_einval_is_returned():
                                                    0, None, o, pd, 65)],
     }
     assert set(cases) == _header_einval_tags()
+    # an empty batch is a no-op, NULL results array included (before any device)
+    pd1 = ctypes.addressof((ctypes.c_int * 1)(0))
+    assert L.yu_csum_batch_uniform(p, 16, 16, 0, 0, None, 0, None, None, None) == 0
+    assert L.yu_csum_batch_ragged(p, po, 0, 1, None, 0, None, None, None) == 0
+    assert L.yu_csum_batch_host_uniform(p, 16, 16, 0, 0, None, 0, None, None, 0) == 0
+    assert L.yu_csum_batch_host_ragged(p, po, 0, 0, None, 0, None, None, 0) == 0
+    assert L.yu_csum_batch_host_iov(ctypes.addressof(iov), ctypes.addressof(first), 0, 0, None, 0, None,
+                                    None, 0) == 0
+    assert L.yu_csum_batch_host_uniform_multi(p, 16, 16, 0, 0, None, 0, None, None, pd1, 1) == 0
     for tag, rcs in cases.items():
         assert all(rc == EINVAL for rc in rcs), (tag, rcs)
     if not torch.cuda.is_available():

@@ -871,6 +871,20 @@ def test_side_stream_and_graph_replay(dev, oracle_c):
         assert np.array_equal(out_r.cpu().numpy(), want_r)
 
 
+def test_empty_batches_are_no_ops(dev):
+    """n == 0 is a no-op returning an empty result, through every front-end call
+    (the C ABI takes a NULL results array then, include/yucsum.h [out])."""
+    d = torch.zeros(64, dtype=torch.uint8, device=dev)
+    assert batch.checksum_uniform(d, 16, 16, 0, "tcp").numel() == 0
+    assert batch.checksum_ragged(d, torch.zeros(1, dtype=torch.int64, device=dev), "udp").numel() == 0
+    assert batch.checksum_ragged(d, torch.zeros(1, dtype=torch.int64, device=dev), "tx_datagram",
+                                 fill=True).numel() == 0
+    h = np.zeros(64, np.uint8)
+    assert batch.checksum_host_uniform(h, 16, 16, 0, "raw").size == 0
+    assert batch.checksum_host_ragged(h, np.zeros(1, np.uint64), "verify_rx").size == 0
+    assert batch.checksum_host_iov([], "raw").size == 0
+
+
 def test_errors_are_loud(dev):
     from yustack_amd._lib import YuError
     d = torch.zeros(1 << 17, dtype=torch.uint8, device=dev)

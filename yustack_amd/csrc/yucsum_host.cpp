@@ -822,8 +822,8 @@ extern "C" int yu_csum_batch_host_uniform(const uint8_t *h_data,
                                           const uint8_t *h_addrs,
                                           uint16_t *h_out, int device) {
   if (bad_mode(mode)) return YU_EINVAL;  // EINVAL:mode
+  if (n == 0) return YU_OK;              // (an empty batch may pass a NULL h_out)
   if (!h_out) return YU_EINVAL;          // EINVAL:out
-  if (n == 0) return YU_OK;
   if (!h_data && len) return YU_EINVAL;                                      // EINVAL:data
   if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;  // EINVAL:len-transport
   if (len > YU_MAX_RAW_LEN) return YU_EINVAL;                                // EINVAL:len-raw
@@ -846,8 +846,8 @@ extern "C" int yu_csum_batch_host_ragged(const uint8_t *h_data,
                                          const uint8_t *h_addrs,
                                          uint16_t *h_out, int device) {
   if (bad_mode(mode)) return YU_EINVAL;  // EINVAL:mode
+  if (n == 0) return YU_OK;              // (an empty batch may pass a NULL h_out)
   if (!h_out) return YU_EINVAL;          // EINVAL:out
-  if (n == 0) return YU_OK;
   if (!h_offsets) return YU_EINVAL;                                   // EINVAL:offsets
   if (!h_data && h_offsets[n] != h_offsets[0]) return YU_EINVAL;     // EINVAL:data
   if (int rc = check_offsets(h_offsets, n, mode)) return rc;
@@ -863,8 +863,8 @@ extern "C" int yu_csum_batch_host_iov(const yu_iovec *iov,
                                       uint16_t initial, const uint8_t *h_addrs,
                                       uint16_t *h_out, int device) {
   if (bad_mode(mode)) return YU_EINVAL;  // EINVAL:mode
+  if (n == 0) return YU_OK;              // (an empty batch may pass a NULL h_out)
   if (!h_out) return YU_EINVAL;          // EINVAL:out
-  if (n == 0) return YU_OK;
   if (!first_iov) return YU_EINVAL;                                   // EINVAL:offsets
   if (!iov && first_iov[n] != first_iov[0]) return YU_EINVAL;        // EINVAL:iov-view
   if (int rc = check_iov(iov, first_iov, n, mode)) return rc;
@@ -881,9 +881,9 @@ extern "C" int yu_csum_batch_host_uniform_multi(const uint8_t *h_data, uint64_t 
                                                 uint16_t *h_out, const int *devices,
                                                 int ndev) {
   if (bad_mode(mode)) return YU_EINVAL;                // EINVAL:mode
-  if (!h_out) return YU_EINVAL;                        // EINVAL:out
   if (bad_devices(devices, ndev)) return YU_EINVAL;    // EINVAL:devices
-  if (n == 0) return YU_OK;
+  if (n == 0) return YU_OK;                            // (h_out may be NULL then)
+  if (!h_out) return YU_EINVAL;                        // EINVAL:out
   if (!h_data && len) return YU_EINVAL;                                      // EINVAL:data
   if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;  // EINVAL:len-transport
   if (len > YU_MAX_RAW_LEN) return YU_EINVAL;                                // EINVAL:len-raw
@@ -903,9 +903,9 @@ extern "C" int yu_csum_batch_host_ragged_multi(const uint8_t *h_data,
                                                uint16_t *h_out, const int *devices,
                                                int ndev) {
   if (bad_mode(mode)) return YU_EINVAL;                // EINVAL:mode
-  if (!h_out) return YU_EINVAL;                        // EINVAL:out
   if (bad_devices(devices, ndev)) return YU_EINVAL;    // EINVAL:devices
-  if (n == 0) return YU_OK;
+  if (n == 0) return YU_OK;                            // (h_out may be NULL then)
+  if (!h_out) return YU_EINVAL;                        // EINVAL:out
   if (!h_offsets) return YU_EINVAL;                                   // EINVAL:offsets
   if (!h_data && h_offsets[n] != h_offsets[0]) return YU_EINVAL;     // EINVAL:data
   if (int rc = check_offsets(h_offsets, n, mode)) return rc;
@@ -925,9 +925,9 @@ extern "C" int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t 
                                             const uint8_t *h_addrs, uint16_t *h_out,
                                             const int *devices, int ndev) {
   if (bad_mode(mode)) return YU_EINVAL;                // EINVAL:mode
-  if (!h_out) return YU_EINVAL;                        // EINVAL:out
   if (bad_devices(devices, ndev)) return YU_EINVAL;    // EINVAL:devices
-  if (n == 0) return YU_OK;
+  if (n == 0) return YU_OK;                            // (h_out may be NULL then)
+  if (!h_out) return YU_EINVAL;                        // EINVAL:out
   if (!first_iov) return YU_EINVAL;                                   // EINVAL:offsets
   if (!iov && first_iov[n] != first_iov[0]) return YU_EINVAL;        // EINVAL:iov-view
   if (int rc = check_iov(iov, first_iov, n, mode)) return rc;

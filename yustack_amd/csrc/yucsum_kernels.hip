@@ -2583,9 +2583,9 @@ bool aligned(const void *p, uintptr_t a) {
 }
 
 int check_common(int mode, const uint16_t *initial_arr, const uint8_t *addrs,
-                 const uint16_t *out, bool fill) {
+                 const uint16_t *out, bool fill, uint64_t n) {
   if (mode < 0 || mode >= YU_MODE_COUNT) return YU_EINVAL;  // EINVAL:mode
-  if (!out && !fill) return YU_EINVAL;                     // EINVAL:out
+  if (!out && !fill && n) return YU_EINVAL;                // EINVAL:out (an empty batch may pass NULL)
   if (fill && !mode_fills(mode)) return YU_EINVAL;         // EINVAL:fill-mode
   if (initial_arr && !aligned(initial_arr, 2)) return YU_EINVAL;  // EINVAL:side-align
   if (addrs && !aligned(addrs, 4)) return YU_EINVAL;              // EINVAL:side-align
@@ -2611,7 +2611,7 @@ int batch_uniform(const uint8_t *data, uint8_t *fill, uint64_t stride,
                   uint32_t len, uint64_t n, int mode,
                   const uint16_t *initial_arr, uint16_t initial,
                   const uint8_t *addrs, uint16_t *out, void *stream) {
-  int rc = check_common(mode, initial_arr, addrs, out, fill != nullptr);
+  int rc = check_common(mode, initial_arr, addrs, out, fill != nullptr, n);
   if (rc) return rc;
   if (n == 0) return YU_OK;
   if (!data) return YU_EINVAL;                                              // EINVAL:data
@@ -2650,7 +2650,7 @@ int batch_ragged(const uint8_t *data, uint8_t *fill, const uint64_t *offsets,
                  uint64_t n, int mode, const uint16_t *initial_arr,
                  uint16_t initial, const uint8_t *addrs, uint16_t *out,
                  void *stream) {
-  int rc = check_common(mode, initial_arr, addrs, out, fill != nullptr);
+  int rc = check_common(mode, initial_arr, addrs, out, fill != nullptr, n);
   if (rc) return rc;
   if (n == 0) return YU_OK;
   if (!offsets || !aligned(offsets, 8)) return YU_EINVAL;  // EINVAL:offsets
