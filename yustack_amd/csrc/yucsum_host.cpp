@@ -220,11 +220,6 @@ class ContextPool {
     std::lock_guard<std::mutex> l(m_);
     for (Ctx *c : idle_) c->release();
   }
-  int created() {
-    std::lock_guard<std::mutex> l(m_);
-    return (int)all_.size();
-  }
-
  private:
   std::mutex m_;
   std::condition_variable cv_;
