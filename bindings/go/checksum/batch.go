@@ -171,6 +171,10 @@ func HostStaging(device int) (pinned, dev uint64) {
 	return uint64(p), uint64(d)
 }
 
+// HostContextPinnedMax is one staging context's pinned bytes at most, between
+// calls (include/yucsum.h YU_HOST_CONTEXT_PINNED_MAX).
+const HostContextPinnedMax = uint64(C.YU_HOST_CONTEXT_PINNED_MAX)
+
 // HostContexts is the bound on staging contexts per device (YU_HOST_CONTEXTS,
 // default 4, read once from the environment).
 func HostContexts() int { return int(C.yu_host_contexts()) }

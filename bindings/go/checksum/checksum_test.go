@@ -76,3 +76,39 @@ func TestShortArgumentsRejected(t *testing.T) {
 		t.Fatal("ragged: short initial accepted")
 	}
 }
+
+// TestStagingIsBounded: goroutines calling at once (the Go runtime spreads them
+// over OS threads) share at most HostContexts() staging contexts, so the pinned
+// staging held afterwards stays within that many contexts' bound
+// (include/yucsum.h, Host-path staging), and a trim frees it.
+func TestStagingIsBounded(t *testing.T) {
+	const n, L = 12000, 1500 // 18 MB: the sliced pipeline
+	data := make([]byte, n*L)
+	for i := range data {
+		data[i] = byte(i * 7)
+	}
+	errs := make(chan error, 32)
+	for g := 0; g < 32; g++ {
+		go func() {
+			out := make([]uint16, n)
+			errs <- BatchHostUniform(data, L, L, n, ModeRaw, nil, nil, out, 0)
+		}()
+	}
+	for g := 0; g < 32; g++ {
+		if err := <-errs; err == ErrNoDevice {
+			t.Skip("no HIP device")
+		} else if err != nil {
+			t.Fatal(err)
+		}
+	}
+	pinned, _ := HostStaging(0)
+	if bound := uint64(HostContexts()) * HostContextPinnedMax; pinned == 0 || pinned > bound {
+		t.Fatalf("pinned staging %d, bound %d", pinned, bound)
+	}
+	if err := HostStagingTrim(0); err != nil {
+		t.Fatal(err)
+	}
+	if pinned, _ = HostStaging(0); pinned != 0 {
+		t.Fatalf("%d pinned bytes after a trim", pinned)
+	}
+}
