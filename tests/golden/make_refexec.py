@@ -365,6 +365,32 @@ def main() -> None:
         sent.append((dg, 17))
         sg = seg if k % 2 else flip(seg)
         add(O.MODE_VERIFY_UDP, sg, a, ref.verify_l4(sg, a[:4], a[4:], 17), "restated")
+    # the UDP field 0x0000 (no RFC 768 0 -> 0xFFFF substitution, header/udp.go:60-62 via
+    # transport/udp/endpoint.go:184): the payload's last word moved by the field value
+    # (one's complement) so that the sum comes to 0xFFFF, then sent again; the executed
+    # sender stores 0x0000. The same for sendTCP, where 0x0000 is legal anyway.
+    def zero_field(send, seg_off, n):
+        data = bytearray(rnd(rng, n))
+        dg = send(bytes(data))
+        f = be16(dg, seg_off)
+        w = (data[-2] << 8 | data[-1]) + f
+        w = w - 0xFFFF if w > 0xFFFF else w
+        data[-2:] = bytes([w >> 8, w & 0xFF])
+        dg = send(bytes(data))
+        assert be16(dg, seg_off) == 0, hex(be16(dg, seg_off))
+        return dg
+    for k in range(6):
+        a = rnd(rng, 8)
+        ports = (rng.getrandbits(16), rng.getrandbits(16))
+        dg = zero_field(lambda d: ref.send_udp(a[:4], a[4:], d, *ports), 26, 2 * rng.randint(1, 40))
+        add(O.MODE_UDP, garble(dg[20:], 6), a, 0)
+        sent.append((dg, 17))
+    for k in range(2):
+        a = rnd(rng, 8)
+        hdr = (rng.getrandbits(16), rng.getrandbits(16), 0x18, rng.getrandbits(32), rng.getrandbits(32), 4096)
+        dg = zero_field(lambda d: ref.send_tcp(a[:4], a[4:], d, *hdr), 36, 2 * rng.randint(1, 40))
+        add(O.MODE_TCP, garble(dg[20:], 16), a, 0)
+        sent.append((dg, 6))
     # ICMP: sendICMPv4 (echo replies and other types), payloads of 0..1600 bytes
     for k in range(50):
         a = rnd(rng, 8)
