@@ -170,7 +170,13 @@ uint16_t yu_pseudo_header_checksum(uint32_t protocol,
  * the checksum field taken as 0 — transport/tcp/connect.go:556-586,
  * header/tcp.go:165-186. Protocol 6. As in every segment sendTCP encodes,
  * 20 <= DataOffset() <= len is required; other segments get an unspecified
- * value (never a fault). */
+ * value (never a fault). Data = the bytes past DataOffset() * 4. (Only
+ * sendTCPWithOptions given options whose length is not a multiple of 4 —
+ * no caller does: sendSynTCP passes 4 or 8, connect.go:266-284 — would sum
+ * its header to the floored DataOffset() and leave the option bytes past it
+ * out of the sum, a value the receiver's check rejects; this mode sums them
+ * as data, as the receiver does. Measured by executing the reference,
+ * DESIGN.md §2.) */
 #define YU_MODE_TCP 2
 /* pkt_i = IPv4 datagram. out[i] = ^IPv4.CalculateChecksum() over
  * b[:IHL*4] (clamped to len) with the header-checksum field taken as 0 —
