@@ -162,18 +162,20 @@ func BatchHostRagged(data []byte, offsets []uint64, mode Mode, initial []uint16,
 
 // HostStaging reports the pinned host and device bytes the host path's staging
 // holds for device now (include/yucsum.h yu_host_staging_bytes). Each call
-// borrows one of at most HostContexts() contexts of its device, so between
-// calls this stays within HostContexts() * YU_HOST_CONTEXT_PINNED_MAX pinned
-// bytes however many OS threads a program's goroutines have run on.
+// borrows one of at most HostContexts() contexts of its device and kind (bulk,
+// or burst for the small direct calls), so between calls this stays within
+// HostContexts() * HostContextPinnedMax pinned bytes however many OS threads a
+// program's goroutines have run on.
 func HostStaging(device int) (pinned, dev uint64) {
 	var d C.uint64_t
 	p := C.yu_host_staging_bytes(C.int(device), &d)
 	return uint64(p), uint64(d)
 }
 
-// HostContextPinnedMax is one staging context's pinned bytes at most, between
-// calls (include/yucsum.h YU_HOST_CONTEXT_PINNED_MAX).
-const HostContextPinnedMax = uint64(C.YU_HOST_CONTEXT_PINNED_MAX)
+// HostContextPinnedMax is the pinned bytes of one bulk and one burst staging
+// context at most, between calls (include/yucsum.h YU_HOST_CONTEXT_PINNED_MAX +
+// YU_HOST_BURST_CONTEXT_PINNED_MAX): HostContexts() of each per device.
+const HostContextPinnedMax = uint64(C.YU_HOST_CONTEXT_PINNED_MAX) + uint64(C.YU_HOST_BURST_CONTEXT_PINNED_MAX)
 
 // HostContexts is the bound on staging contexts per device (YU_HOST_CONTEXTS,
 // default 4, read once from the environment).

@@ -400,29 +400,39 @@ int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t *first_iov,
 
 /* A host call borrows one staging context of its device for its own length
  * and returns it; a caller that finds every context in use waits for one.
- * Contexts are created on first need, up to yu_host_contexts() per device:
- * YU_HOST_CONTEXTS in the environment (1..64, default 4; a product setting,
- * read without the YU_TUNING gate). So the staging grows with the calls the
- * pool lets run at once, not with the number of OS threads that ever called
- * (the Go consumer calls from many goroutines, which migrate across OS
- * threads: transport/tcp/accept.go:238, transport/tcp/endpoint.go:229,
- * network/ipv4/icmp.go:30-34).
+ * There are two pools per device: bulk contexts (3 pipeline slots) and burst
+ * contexts (1 slot) for the calls that take the direct path (one slice of at
+ * most 4 MiB: a tun read burst), so a burst never waits behind bulk batches
+ * that hold every bulk context. Contexts are created on first need, up to
+ * yu_host_contexts() per pool and device: YU_HOST_CONTEXTS in the environment
+ * (1..64, default 4; a product setting, read without the YU_TUNING gate). So
+ * the staging grows with the calls the pools let run at once, not with the
+ * number of OS threads that ever called (the Go consumer calls from many
+ * goroutines, which migrate across OS threads: transport/tcp/accept.go:238,
+ * transport/tcp/endpoint.go:229, network/ipv4/icmp.go:30-34).
  *
- * A context holds 3 pipeline slots of at most one slice each: up to
+ * A bulk context holds 3 pipeline slots of at most one slice each: up to
  * YU_HOST_SLICE_BYTES of packet bytes and YU_HOST_SLICE_PACKETS packets'
- * side arrays. Between calls a device's staging is therefore at most
- * yu_host_contexts() * YU_HOST_CONTEXT_PINNED_MAX bytes of pinned host memory
- * and yu_host_contexts() * YU_HOST_CONTEXT_DEVICE_MAX of device memory (a
- * packet longer than a slice gets a slice of its own for that call; the
- * context gives the extra back when the call returns). */
+ * side arrays; a burst context one slot of at most 4 MiB and as many
+ * packets. Between calls a device's staging is therefore at most
+ * yu_host_contexts() * (YU_HOST_CONTEXT_PINNED_MAX +
+ * YU_HOST_BURST_CONTEXT_PINNED_MAX) bytes of pinned host memory and
+ * yu_host_contexts() * (YU_HOST_CONTEXT_DEVICE_MAX +
+ * YU_HOST_BURST_CONTEXT_DEVICE_MAX) of device memory (a packet longer than a
+ * slice gets a slice of its own for that call; the context gives the extra
+ * back when the call returns). */
 #define YU_HOST_SLICE_BYTES (32ull << 20)
 #define YU_HOST_SLICE_PACKETS (1ull << 18)
 #define YU_HOST_CONTEXT_PINNED_MAX \
   (3ull * (YU_HOST_SLICE_BYTES + 26ull * YU_HOST_SLICE_PACKETS + 72ull))
 #define YU_HOST_CONTEXT_DEVICE_MAX \
   (3ull * (YU_HOST_SLICE_BYTES + 22ull * YU_HOST_SLICE_PACKETS + 8ull))
+#define YU_HOST_BURST_CONTEXT_PINNED_MAX \
+  ((4ull << 20) + 26ull * YU_HOST_SLICE_PACKETS + 72ull)
+#define YU_HOST_BURST_CONTEXT_DEVICE_MAX \
+  ((4ull << 20) + 22ull * YU_HOST_SLICE_PACKETS + 8ull)
 
-/* The pool bound K (YU_HOST_CONTEXTS, clamped to 1..64). */
+/* The pool bound K (YU_HOST_CONTEXTS, clamped to 1..64), per pool. */
 int yu_host_contexts(void);
 /* Pinned host bytes the host-path staging of `device` holds now (idle and
  * lent contexts); the device bytes go to *dev_bytes when it is not NULL.

@@ -325,9 +325,10 @@ static void test_gpu_batches() {
     for (auto &th : ts) th.join();
     EXPECT(bad == 0, "16 threads through the host staging pool: %d bad calls", bad.load());
     const batch::Staging st = batch::HostStaging(0);
-    EXPECT(st.pinned > 0 && st.pinned <= (uint64_t)batch::HostContexts() * YU_HOST_CONTEXT_PINNED_MAX,
+    const uint64_t k = (uint64_t)batch::HostContexts();
+    EXPECT(st.pinned > 0 && st.pinned <= k * (YU_HOST_CONTEXT_PINNED_MAX + YU_HOST_BURST_CONTEXT_PINNED_MAX),
            "pinned staging %lu within the pool bound", (unsigned long)st.pinned);
-    EXPECT(st.device <= (uint64_t)batch::HostContexts() * YU_HOST_CONTEXT_DEVICE_MAX,
+    EXPECT(st.device <= k * (YU_HOST_CONTEXT_DEVICE_MAX + YU_HOST_BURST_CONTEXT_DEVICE_MAX),
            "device staging %lu within the pool bound", (unsigned long)st.device);
     batch::HostStagingTrim(0);
     EXPECT(batch::HostStaging(0).pinned == 0, "trim frees the idle staging");

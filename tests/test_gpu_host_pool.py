@@ -78,8 +78,8 @@ def test_many_threads_share_a_bounded_pool(dev, oracle_c):
     assert not errors, errors[:5]
     pinned, devb = _lib.host_staging(0)
     print(f"K={K}: staging after 64 threads: pinned {pinned / 2**20:.1f} MiB, device {devb / 2**20:.1f} MiB")
-    assert 0 < pinned <= K * _lib.HOST_CONTEXT_PINNED_MAX
-    assert 0 < devb <= K * _lib.HOST_CONTEXT_DEVICE_MAX
+    assert 0 < pinned <= K * (_lib.HOST_CONTEXT_PINNED_MAX + _lib.HOST_BURST_CONTEXT_PINNED_MAX)
+    assert 0 < devb <= K * (_lib.HOST_CONTEXT_DEVICE_MAX + _lib.HOST_BURST_CONTEXT_DEVICE_MAX)
     assert _lib.lib().yu_host_staging_trim(0) == 0
     assert _lib.host_staging(0) == (0, 0)
     # the pool still serves calls after a trim
@@ -108,7 +108,8 @@ ts = [threading.Thread(target=go) for _ in range(8)]
 [t.start() for t in ts]
 [t.join() for t in ts]
 p, d = _lib.host_staging(0)
-assert not bad and 0 < p <= _lib.HOST_CONTEXT_PINNED_MAX and d <= _lib.HOST_CONTEXT_DEVICE_MAX, (bad, p, d)
+assert not bad and 0 < p <= _lib.HOST_CONTEXT_PINNED_MAX + _lib.HOST_BURST_CONTEXT_PINNED_MAX, (bad, p, d)
+assert d <= _lib.HOST_CONTEXT_DEVICE_MAX + _lib.HOST_BURST_CONTEXT_DEVICE_MAX, d
 print("ok", p, d)
 """
 
@@ -121,3 +122,51 @@ def test_one_context_serialises_callers(dev):
                        timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.startswith("ok")
+
+
+def test_bursts_do_not_wait_behind_bulk_batches(dev, oracle_c):
+    """Six threads keep every bulk context busy with 384 MB pipelined batches (each
+    several milliseconds of PCIe) while the main thread sends 64-packet bursts; a
+    burst takes the direct path through its own pool (include/yucsum.h), so none waits
+    for a bulk call to finish: every burst is bit-exact and the slowest one stays far
+    below one bulk call."""
+    import time
+    rng = np.random.default_rng(65)
+    n_big = 256000
+    big = rng.integers(0, 256, size=n_big * 1500, dtype=np.uint8)
+    small, small_a = _tcp_batch(rng, 64)
+    want = oracle_c.batch(small, O.MODE_TCP, stride=1500, length=1500, n=64, addrs=small_a)
+    stop = threading.Event()
+    bulk_times, errors = [], []
+
+    def bulk():
+        out = np.empty(n_big, np.uint16)
+        while not stop.is_set():
+            t0 = time.perf_counter()
+            try:
+                batch.checksum_host_uniform(big, 1500, 1500, n_big, "raw", out=out)
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+                return
+            bulk_times.append(time.perf_counter() - t0)
+
+    threads = [threading.Thread(target=bulk) for _ in range(6)]
+    for t in threads:
+        t.start()
+    time.sleep(0.2)  # the bulk calls hold every bulk context by now
+    lat, bad = [], 0
+    for _ in range(200):
+        t0 = time.perf_counter()
+        got = batch.checksum_host_uniform(small, 1500, 1500, 64, "tcp", addrs=small_a)
+        lat.append(time.perf_counter() - t0)
+        bad += not np.array_equal(got, want)
+    stop.set()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors and not bad, (errors, bad)
+    lat.sort()
+    typical_bulk = sorted(bulk_times)[len(bulk_times) // 2]
+    print(f"bursts under bulk load: median {lat[100] * 1e6:.0f} us, max {lat[-1] * 1e6:.0f} us; "
+          f"a bulk call {typical_bulk * 1e3:.1f} ms")
+    assert len(bulk_times) >= 6
+    assert lat[-1] < typical_bulk / 2, (lat[-1], typical_bulk)

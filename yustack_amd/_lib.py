@@ -30,6 +30,8 @@ EXPORTS = (
 HOST_SLICE_BYTES, HOST_SLICE_PACKETS = 32 << 20, 1 << 18
 HOST_CONTEXT_PINNED_MAX = 3 * (HOST_SLICE_BYTES + 26 * HOST_SLICE_PACKETS + 72)
 HOST_CONTEXT_DEVICE_MAX = 3 * (HOST_SLICE_BYTES + 22 * HOST_SLICE_PACKETS + 8)
+HOST_BURST_CONTEXT_PINNED_MAX = (4 << 20) + 26 * HOST_SLICE_PACKETS + 72
+HOST_BURST_CONTEXT_DEVICE_MAX = (4 << 20) + 22 * HOST_SLICE_PACKETS + 8
 
 YU_OK, YU_EINVAL, YU_ENODEV, YU_ENOMEM, YU_EHIP_BASE = 0, -22, -19, -12, -1000
 

@@ -49,8 +49,8 @@ namespace {
 
 constexpr int kSlots = 3;
 constexpr uint64_t kSliceBytes = YU_HOST_SLICE_BYTES;  // 32 MiB
-// Packets per slice at most: bounds a slot's side arrays (34 bytes of pinned and
-// 30 of device memory per packet) as kSliceBytes bounds its packet bytes. Only
+// Packets per slice at most: bounds a slot's side arrays (26 bytes of pinned and
+// 22 of device memory per packet) as kSliceBytes bounds its packet bytes. Only
 // packets under 128 bytes reach it; 256K of 64-byte packets is 16 MiB, still
 // hundreds of microseconds of PCIe per slice.
 constexpr uint64_t kSlicePkts = YU_HOST_SLICE_PACKETS;  // 256K
@@ -88,25 +88,32 @@ struct Slot {
 // Staging bytes of a context reserved for (data_bytes, pk): pinned host and device.
 // (the allocations of Ctx::reserve: packet bytes, addrs 8, initial 2, results 4,
 // offsets 8, coherent results 4 per packet, one more offset, the 64-byte flag)
-constexpr uint64_t pinned_bytes(uint64_t data_bytes, uint64_t pk) {
-  return kSlots * ((data_bytes ? data_bytes : 16) + pk * 8 + pk * 2 + pk * 4 + (pk + 1) * 8 + pk * 4 + 64);
+constexpr uint64_t pinned_bytes(uint64_t data_bytes, uint64_t pk, int slots = kSlots) {
+  return slots * ((data_bytes ? data_bytes : 16) + pk * 8 + pk * 2 + pk * 4 + (pk + 1) * 8 + pk * 4 + 64);
 }
-constexpr uint64_t device_bytes(uint64_t data_bytes, uint64_t pk) {
-  return kSlots * ((data_bytes ? data_bytes : 16) + pk * 8 + pk * 2 + pk * 4 + (pk + 1) * 8);
+constexpr uint64_t device_bytes(uint64_t data_bytes, uint64_t pk, int slots = kSlots) {
+  return slots * ((data_bytes ? data_bytes : 16) + pk * 8 + pk * 2 + pk * 4 + (pk + 1) * 8);
 }
+// The default direct cut-over (bytes of one burst that the kernel reads from
+// host memory itself; see `direct` below).
+constexpr uint64_t kDirectMax = 4ull << 20;
 static_assert(pinned_bytes(kSliceBytes, kSlicePkts) == YU_HOST_CONTEXT_PINNED_MAX, "yucsum.h bound");
 static_assert(device_bytes(kSliceBytes, kSlicePkts) == YU_HOST_CONTEXT_DEVICE_MAX, "yucsum.h bound");
+static_assert(pinned_bytes(kDirectMax, kSlicePkts, 1) == YU_HOST_BURST_CONTEXT_PINNED_MAX, "yucsum.h bound");
+static_assert(device_bytes(kDirectMax, kSlicePkts, 1) == YU_HOST_BURST_CONTEXT_DEVICE_MAX, "yucsum.h bound");
 static_assert(kSlots == 3, "yucsum.h bounds assume 3 slots");
 
 struct Ctx {
   int dev = -1;
+  int nslots = kSlots;  // 1 for a burst context (the direct path uses slot 0 alone)
   // (atomic: yu_host_staging_bytes reads them while the holder may reserve)
   std::atomic<uint64_t> cap_data{0}, cap_pk{0};
   std::atomic<bool> reserved{false};
   Slot s[kSlots];
 
   void release() {
-    for (Slot &x : s) {
+    for (int k = 0; k < nslots; ++k) {
+      Slot &x = s[k];
       if (x.h_data) (void)hipHostFree(x.h_data);
       if (x.h_addrs) (void)hipHostFree(x.h_addrs);
       if (x.h_init) (void)hipHostFree(x.h_init);
@@ -136,7 +143,8 @@ struct Ctx {
     if (pk < cap_pk) pk = cap_pk;
     release();
     reserved = true;  // (partly) allocated: release() frees what a failure left
-    for (Slot &x : s) {
+    for (int k = 0; k < nslots; ++k) {
+      Slot &x = s[k];
       YU_TRY(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
       YU_TRY(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
       YU_TRY(hipHostMalloc((void **)&x.h_data, data_bytes ? data_bytes : 16, 0));
@@ -180,7 +188,8 @@ int host_contexts() {
 // HIP runtime may already be gone); an idle one is lent to the next caller.
 class ContextPool {
  public:
-  Ctx *acquire(int dev) {
+  // slots: kSlots (bulk pool) or 1 (burst pool)
+  Ctx *acquire(int dev, int slots) {
     std::unique_lock<std::mutex> l(m_);
     cv_.wait(l, [&] { return !idle_.empty() || (int)all_.size() < host_contexts(); });
     Ctx *c;
@@ -191,14 +200,17 @@ class ContextPool {
       all_.push_back(new Ctx());
       c = all_.back();
       c->dev = dev;
+      c->nslots = slots;
     }
     return c;
   }
-  // A context that grew past one standard slice (a packet longer than
-  // kSliceBytes is a slice of its own) gives that memory back here, so the pool
-  // keeps at most host_contexts() x one standard slot budget between calls.
+  // A context that grew past its standard size (a packet longer than
+  // kSliceBytes is a slice of its own; a burst context that served a fallback or
+  // a tuned, larger direct cut-over) gives that memory back here, so the pools
+  // keep at most host_contexts() x their standard budgets between calls.
   void give_back(Ctx *c) {
-    if (c->cap_data > kSliceBytes || c->cap_pk > kSlicePkts) c->release();
+    const uint64_t cap = c->nslots == kSlots ? kSliceBytes : kDirectMax;
+    if (c->cap_data > cap || c->cap_pk > kSlicePkts) c->release();
     {
       std::lock_guard<std::mutex> l(m_);
       idle_.push_back(c);
@@ -211,8 +223,8 @@ class ContextPool {
     pinned = dev = 0;
     for (Ctx *c : all_) {
       if (!c->reserved) continue;
-      pinned += pinned_bytes(c->cap_data, c->cap_pk);
-      dev += device_bytes(c->cap_data, c->cap_pk);
+      pinned += pinned_bytes(c->cap_data, c->cap_pk, c->nslots);
+      dev += device_bytes(c->cap_data, c->cap_pk, c->nslots);
     }
   }
   // Frees the staging of every idle context (lent ones are left alone).
@@ -226,9 +238,14 @@ class ContextPool {
   std::vector<Ctx *> all_, idle_;
 };
 
-ContextPool &pool_of(int device) {
-  static ContextPool *pools = new ContextPool[64];  // process lifetime
-  return pools[device];
+// Two pools per device: bulk contexts (3 slots, any call) and burst contexts (1
+// slot, calls that take the direct path), so a tun burst never waits behind
+// bulk batches that hold every bulk context.
+enum PoolKind { kBulk = 0, kBurst = 1 };
+
+ContextPool &pool_of(int device, int kind) {
+  static ContextPool *pools = new ContextPool[2 * 64];  // process lifetime
+  return pools[2 * device + kind];
 }
 
 // Staging copies of pageable input. One thread's memcpy into pinned memory
@@ -346,7 +363,8 @@ int finish(Slot &x, uint16_t *h_out) {
 // on every exit path).
 class Lease {
  public:
-  explicit Lease(int device) : device_(device), c_(pool_of(device).acquire(device)) {
+  Lease(int device, int kind)
+      : device_(device), kind_(kind), c_(pool_of(device, kind).acquire(device, kind == kBurst ? 1 : kSlots)) {
     // A previous call that failed midway may have left slices in flight:
     // drain them without copying (their h_out belonged to that call).
     for (Slot &x : c_->s) {
@@ -354,13 +372,13 @@ class Lease {
       x.busy = false;
     }
   }
-  ~Lease() { pool_of(device_).give_back(c_); }
+  ~Lease() { pool_of(device_, kind_).give_back(c_); }
   Lease(const Lease &) = delete;
   Lease &operator=(const Lease &) = delete;
   Ctx &ctx() { return *c_; }
 
  private:
-  int device_;
+  int device_, kind_;
   Ctx *c_;
 };
 
@@ -378,7 +396,7 @@ constexpr int kNoDirect = 1;  // not an error: take the pipelined path
 uint64_t direct_max() {
   static const uint64_t v = [] {
     const char *e = yu::tuning_env("YU_HOST_DIRECT_MAX");
-    return e && *e ? strtoull(e, nullptr, 10) : (uint64_t)(4ull << 20);
+    return e && *e ? strtoull(e, nullptr, 10) : kDirectMax;
   }();
   return v;
 }
@@ -448,8 +466,11 @@ template <class Layout>
 int run_slices(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
                const uint8_t *h_addrs, uint16_t *h_out, bool pin_out);
 
+// One host batch on the current device: its slices' geometry first (no context
+// needed), then a context from the burst pool when the batch takes the direct
+// path (one slice of at most direct_max() bytes) or from the bulk pool otherwise.
 template <class Layout>
-int pipeline(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
+int pipeline(int device, const Layout &L, uint64_t n, const uint16_t *h_init,
              const uint8_t *h_addrs, uint16_t *h_out) {
   // capacity: the largest slice of this batch
   uint64_t max_b = 0, max_pk = 0;
@@ -460,17 +481,23 @@ int pipeline(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
     if (cnt > max_pk) max_pk = cnt;
     first += cnt;
   }
+  const bool burst = max_pk == n && max_b <= direct_max();
+  Lease lease(device, burst ? kBurst : kBulk);
+  Ctx &c = lease.ctx();
   int rc = c.reserve(max_b, max_pk);
   if (rc) return rc;
   rc = kNoDirect;
-  if (max_pk == n && max_b <= direct_max()) rc = direct(c.s[0], L, n, h_init, h_addrs, h_out);
+  if (burst) rc = direct(c.s[0], L, n, h_init, h_addrs, h_out);
+  // (a burst whose memory cannot be mapped for the kernel falls back to the copies,
+  // through its context's one slot)
   if (rc == kNoDirect) rc = run_slices(c, L, n, h_init, h_addrs, h_out, is_pinned(h_out));
   if (rc) {
     // A failed call returns with no transfer still aimed at the caller's
     // buffers: every slot's stream is drained before the error goes back (a
     // pinned input is read, and a pinned h_out written, by the copies
     // themselves, including those of a slice that failed halfway).
-    for (Slot &x : c.s) {
+    for (int k = 0; k < c.nslots; ++k) {
+      Slot &x = c.s[k];
       if (x.st) (void)hipStreamSynchronize(x.st);
       x.busy = false;
     }
@@ -484,9 +511,9 @@ int run_slices(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
                const uint8_t *h_addrs, uint16_t *h_out, bool pin_out) {
   int rc = YU_OK;
   const uint64_t outs = YU_MODE_OUTPUTS(L.mode);  // results per packet
-  uint64_t k = 0;                                 // slice counter: slot k % kSlots
+  uint64_t k = 0;                                 // slice counter: slot k % nslots
   for (uint64_t first = 0; first < n; ++k) {
-    Slot &x = c.s[k % kSlots];
+    Slot &x = c.s[k % (uint64_t)c.nslots];
     rc = finish(x, h_out);
     if (rc) return rc;
     const uint64_t cnt = L.count(first);
@@ -519,8 +546,8 @@ int run_slices(Ctx &c, const Layout &L, uint64_t n, const uint16_t *h_init,
     x.busy = true;
     first += cnt;
   }
-  for (Slot &x : c.s) {
-    rc = finish(x, h_out);
+  for (int j = 0; j < c.nslots; ++j) {
+    rc = finish(c.s[j], h_out);
     if (rc) return rc;
   }
   return YU_OK;
@@ -659,11 +686,7 @@ int on_device(int device, F &&f) {
   int prev = 0;
   YU_TRY(hipGetDevice(&prev));
   YU_TRY(hipSetDevice(device));
-  int rc;
-  {
-    Lease lease(device);
-    rc = f(lease.ctx());
-  }
+  const int rc = f();
   (void)hipSetDevice(prev);
   return rc;
 }
@@ -823,14 +846,14 @@ extern "C" int yu_csum_batch_host_uniform(const uint8_t *h_data,
   if (mode != YU_MODE_RAW && len > YU_MAX_TRANSPORT_LEN) return YU_EINVAL;  // EINVAL:len-transport
   if (len > YU_MAX_RAW_LEN) return YU_EINVAL;                                // EINVAL:len-raw
   if (span_wraps(h_data, stride, len, n)) return YU_EINVAL;                  // EINVAL:span
-  return on_device(device, [&](Ctx &c) {
+  return on_device(device, [&] {
     const uint64_t pstride = stride ? stride : 1;
     uint64_t slice = kSliceBytes / pstride;
     if (slice > kSlicePkts) slice = kSlicePkts;
     if (slice < 1) slice = 1;
     if (slice > n) slice = n;
     UniformLayout L{h_data, stride, n, slice, len, mode, initial, is_pinned(h_data)};
-    return pipeline(c, L, n, h_initial_arr, h_addrs, h_out);
+    return pipeline(device, L, n, h_initial_arr, h_addrs, h_out);
   });
 }
 
@@ -846,9 +869,9 @@ extern "C" int yu_csum_batch_host_ragged(const uint8_t *h_data,
   if (!h_offsets) return YU_EINVAL;                                   // EINVAL:offsets
   if (!h_data && h_offsets[n] != h_offsets[0]) return YU_EINVAL;     // EINVAL:data
   if (int rc = check_offsets(h_offsets, n, mode)) return rc;
-  return on_device(device, [&](Ctx &c) {
+  return on_device(device, [&] {
     RaggedLayout L{h_data, h_offsets, n, mode, initial, is_pinned(h_data)};
-    return pipeline(c, L, n, h_initial_arr, h_addrs, h_out);
+    return pipeline(device, L, n, h_initial_arr, h_addrs, h_out);
   });
 }
 
@@ -863,9 +886,9 @@ extern "C" int yu_csum_batch_host_iov(const yu_iovec *iov,
   if (!first_iov) return YU_EINVAL;                                   // EINVAL:offsets
   if (!iov && first_iov[n] != first_iov[0]) return YU_EINVAL;        // EINVAL:iov-view
   if (int rc = check_iov(iov, first_iov, n, mode)) return rc;
-  return on_device(device, [&](Ctx &c) {
+  return on_device(device, [&] {
     IovLayout L{iov, first_iov, n, mode, initial};
-    return pipeline(c, L, n, h_initial_arr, h_addrs, h_out);
+    return pipeline(device, L, n, h_initial_arr, h_addrs, h_out);
   });
 }
 
@@ -936,7 +959,12 @@ extern "C" int yu_csum_batch_host_iov_multi(const yu_iovec *iov, const uint64_t 
 
 extern "C" uint64_t yu_host_staging_bytes(int device, uint64_t *dev_bytes) {
   uint64_t pinned = 0, dev = 0;
-  if (device >= 0 && device < 64) pool_of(device).held(pinned, dev);
+  for (int kind : {kBulk, kBurst}) {
+    uint64_t p = 0, d = 0;
+    if (device >= 0 && device < 64) pool_of(device, kind).held(p, d);
+    pinned += p;
+    dev += d;
+  }
   if (dev_bytes) *dev_bytes = dev;
   return pinned;
 }
@@ -951,7 +979,8 @@ extern "C" int yu_host_staging_trim(int device) {
     (void)hipGetLastError();
     return YU_ENODEV;
   }
-  pool_of(device).trim();
+  pool_of(device, kBulk).trim();
+  pool_of(device, kBurst).trim();
   if (restore) (void)hipSetDevice(prev);
   return YU_OK;
 }
