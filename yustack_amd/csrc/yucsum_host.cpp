@@ -17,11 +17,13 @@
 // slot while the previous slices are on the GPU. A batch of at most 4 MiB
 // (a tun read burst) skips the copies instead: the kernel reads the pinned
 // host memory and writes the results there over PCIe (see `direct`), which
-// more than halves the per-call latency. Staging lives in a bounded per-device
-// pool of contexts (ContextPool: at most YU_HOST_CONTEXTS of them, default 4,
-// each 3 slots of at most one slice), checked out for the length of one call and
-// returned: concurrent callers share nothing while they hold one, and a caller
-// that finds every context of its device in use waits for one. Memory therefore
+// more than halves the per-call latency. Staging lives in two bounded pools of
+// contexts per device (ContextPool: at most YU_HOST_CONTEXTS of each, default 4;
+// bulk contexts of 3 slots of at most one slice, burst contexts of one slot for
+// the direct calls), checked out for the length of one call and returned:
+// concurrent callers share nothing while they hold one, a caller that finds
+// every context of its kind in use waits for one, and a burst never waits behind
+// bulk batches. Memory therefore
 // grows with the number of concurrent calls the pool allows, not with the
 // number of OS threads that ever called (a Go caller's goroutines migrate over
 // many of them); yu_host_staging_bytes reports it.
