@@ -332,8 +332,9 @@ inline void FillHostPackets(const yu_iovec *iov, const uint64_t *first_iov, uint
 }
 
 // Host-path staging of `device` (include/yucsum.h, "Host-path staging"): the pinned
-// and device bytes its bounded context pool holds now; at most HostContexts() x
-// YU_HOST_CONTEXT_PINNED_MAX / _DEVICE_MAX between calls.
+// and device bytes its bounded context pools hold now; at most HostContexts() x
+// (YU_HOST_CONTEXT_PINNED_MAX + YU_HOST_BURST_CONTEXT_PINNED_MAX) pinned and the
+// _DEVICE_MAX sums on the device between calls (bulk and burst contexts).
 struct Staging {
   uint64_t pinned, device;
 };

@@ -372,6 +372,8 @@ def test_host_staging_pool_bound_and_setting():
     src = open(HEADER).read()
     assert "#define YU_HOST_SLICE_BYTES (32ull << 20)" in src and "#define YU_HOST_SLICE_PACKETS (1ull << 18)" in src
     assert _lib.HOST_CONTEXT_PINNED_MAX == 3 * ((32 << 20) + 26 * (1 << 18) + 72)  # ~115.5 MiB
+    assert _lib.HOST_BURST_CONTEXT_PINNED_MAX == (4 << 20) + 26 * (1 << 18) + 72  # ~10.5 MiB, one slot
+    assert _lib.HOST_BURST_CONTEXT_DEVICE_MAX == (4 << 20) + 22 * (1 << 18) + 8
     probe = f"import sys; sys.path.insert(0, {ROOT!r}); from yustack_amd import _lib; print(_lib.lib().yu_host_contexts())"
     for val, want in ((None, 4), ("2", 2), ("0", 1), ("100", 64), ("junk", 4)):
         env = {k: v for k, v in os.environ.items() if not k.startswith("YU_")}
