@@ -129,13 +129,16 @@ def test_bursts_do_not_wait_behind_bulk_batches(dev, oracle_c):
     several milliseconds of PCIe) while the main thread sends 64-packet bursts; a
     burst takes the direct path through its own pool (include/yucsum.h), so none waits
     for a bulk call to finish: every burst is bit-exact and the slowest one stays far
-    below one bulk call."""
+    below one bulk call (measured: median 39 us, slowest 5.9 ms with the context's creation
+    inside the timed calls, against 40 ms per bulk call)."""
     import time
     rng = np.random.default_rng(65)
     n_big = 256000
     big = rng.integers(0, 256, size=n_big * 1500, dtype=np.uint8)
     small, small_a = _tcp_batch(rng, 64)
     want = oracle_c.batch(small, O.MODE_TCP, stride=1500, length=1500, n=64, addrs=small_a)
+    # the burst context exists before the bulk load starts (creating it is not the point)
+    assert np.array_equal(batch.checksum_host_uniform(small, 1500, 1500, 64, "tcp", addrs=small_a), want)
     stop = threading.Event()
     bulk_times, errors = [], []
 
