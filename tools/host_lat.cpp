@@ -27,6 +27,23 @@ __global__ void flag_kernel(volatile unsigned *flag, unsigned v) {
   __threadfence_system();
 }
 
+// The flag written by the kernel itself: the last of its blocks to finish
+// (device-scope counter, reset by that block) stores it, so no second launch.
+__global__ void empty_then_flag(unsigned *ctr, volatile unsigned *flag, unsigned v) {
+  __shared__ bool last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(ctr, 1u) == gridDim.x - 1u;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    *ctr = 0u;
+    __threadfence_system();
+    *flag = v;
+  }
+}
+
 template <class F>
 static double per_call_us(int reps, F &&f) {
   for (int i = 0; i < 20; ++i) f();
@@ -96,6 +113,26 @@ int main() {
            }
          }));
   CK(hipStreamSynchronize(st));
+  printf("empty launch + hipStreamWriteValue32 + poll: %6.2f us\n", per_call_us(reps, [&] {
+           ++seq;
+           empty_kernel<<<1, 64, 0, st>>>(nullptr);
+           (void)hipStreamWriteValue32(st, flag, seq, 0);
+           while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+           }
+         }));
+  CK(hipStreamSynchronize(st));
+  unsigned *ctr;
+  CK(hipMalloc((void **)&ctr, 4));
+  CK(hipMemset(ctr, 0, 4));
+  for (int blocks : {1, 64, 1024}) {
+    printf("kernel (%4d blocks) storing the flag itself + poll: %6.2f us\n", blocks, per_call_us(reps, [&] {
+             ++seq;
+             empty_then_flag<<<blocks, 256, 0, st>>>(ctr, flag, seq);
+             while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+             }
+           }));
+    CK(hipStreamSynchronize(st));
+  }
   printf("batch kernel + flag kernel + poll: %6.2f us\n", per_call_us(reps, [&] {
            ++seq;
            (void)yu_csum_batch_uniform(pinned, L, L, n, YU_MODE_TCP, nullptr, 0, addrs, out, st);
