@@ -440,7 +440,9 @@ def burst_crossover(L: int = 1500) -> dict:
       one L-byte packet (a C caller adds ~2 ns per call, a cgo caller ~100 ns);
     * the batched host path, yu_csum_batch_host_ragged (BatchHostRagged in Go), RAW
       mode (Checksum(pkt, initial) per packet) on bursts of L-byte packets packed back
-      to back, per call, from pageable memory (a Go heap buffer) and from pinned;
+      to back, per call, from pageable memory (a Go heap buffer) and from pinned,
+      called straight through the C ABI (ctypes, pointers taken once: ~1 us of call
+      overhead, close to a cgo caller's) and checked against the scalar drop-in;
     * the burst size above which one batched call beats that many scalar calls: the
       first measured burst where it does, and k* where the straight line through that
       burst's time and the one before it meets k * s, s being the scalar cost of one
@@ -466,16 +468,25 @@ def burst_crossover(L: int = 1500) -> dict:
     init = rng.integers(0, 65536, size=nmax, dtype=np.uint16)
     for kind, blob in (("pageable", blob_np), ("pinned", blob_pin)):
         us = []
+        src = blob.ctypes.data if kind == "pageable" else blob.data_ptr()
         for k in CROSSOVER_BURSTS:
             offs = np.arange(k + 1, dtype=np.uint64) * L
             o = np.empty(k, np.uint16)
+            # straight through the C ABI with the pointers taken once, as a cgo or C++
+            # caller makes the call (the Python wrapper's argument checks add ~4 us)
+            args = (src, offs.ctypes.data, k, batch.MODES["raw"], init.ctypes.data, 0, None, o.ctypes.data, 0)
             for _ in range(10):
-                batch.checksum_host_ragged(blob, offs, "raw", initial_arr=init[:k], out=o)
+                rc = L_.yu_csum_batch_host_ragged(*args)
+            if rc:
+                raise RuntimeError(f"yu_csum_batch_host_ragged: {rc}")
             n = 300
             t0 = time.perf_counter()
             for _ in range(n):
-                batch.checksum_host_ragged(blob, offs, "raw", initial_arr=init[:k], out=o)
+                L_.yu_csum_batch_host_ragged(*args)
             us.append((time.perf_counter() - t0) / n * 1e6)
+            if k == 64:  # the batched results equal the scalar drop-in's, packet by packet
+                ok = all(int(o[i]) == L_.yu_checksum(src + i * L, L, int(init[i])) for i in range(k))
+                res[f"{kind}_matches_scalar"] = ok
         res[f"host_ragged_{kind}_us_per_call"] = [round(u, 2) for u in us]
         cross = None
         for j, (k, u) in enumerate(zip(CROSSOVER_BURSTS, us)):
