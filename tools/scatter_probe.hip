@@ -34,6 +34,37 @@ __global__ void scatter_block(uint8_t *d, uint64_t stride, uint64_t n, uint32_t 
   }
 }
 
+// W-byte aligned block holding each field, READ, patched with the field's two
+// bytes (big-endian v[i]) and written back whole by W/16 lanes: the real bytes of
+// a two-pass in-place writer (pass 1 read-only results, pass 2 this)
+template <int W, bool NTS>
+__global__ void rmw_block(uint8_t *d, uint64_t stride, uint64_t n, uint32_t f, const uint16_t *v) {
+  constexpr int L = W / 16;
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  for (uint64_t i = t / L; i < n; i += (uint64_t)gridDim.x * blockDim.x / L) {
+    uint8_t *fp = d + i * stride + f;
+    uint4 *q = (uint4 *)(((uintptr_t)fp) & ~(uintptr_t)(W - 1)) + (t % L);
+    uint4 x = *q;
+    const uint64_t off = (uint64_t)(fp - (uint8_t *)q);  // < 16: this lane holds the field
+    if (off < 16u) {
+      const uint32_t be = (uint32_t)((v[i] >> 8) | ((v[i] & 0xFFu) << 8));
+      const uint32_t sh = 8u * (uint32_t)(off & 3u), m = 0xFFFFu << sh;
+      const uint32_t k = (uint32_t)(off >> 2);
+      uint32_t w = k == 0 ? x.x : (k == 1 ? x.y : (k == 2 ? x.z : x.w));
+      w = (w & ~m) | (be << sh);
+      if (k == 0) x.x = w; else if (k == 1) x.y = w; else if (k == 2) x.z = w; else x.w = w;
+    }
+    if (NTS) {
+      __builtin_nontemporal_store(x.x, &q->x);
+      __builtin_nontemporal_store(x.y, &q->y);
+      __builtin_nontemporal_store(x.z, &q->z);
+      __builtin_nontemporal_store(x.w, &q->w);
+    } else {
+      *q = x;
+    }
+  }
+}
+
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 __global__ void readall(const u4v *d, uint64_t n16, uint32_t *sink) {
   uint32_t s = 0;
@@ -93,5 +124,18 @@ int main(int argc, char **argv) {
     readall<<<grid, 256>>>((const u4v *)d[r & 1], bytes / 16, sink);
     scatter_block<256><<<grid, 256>>>(d[r & 1], stride, n, 16);
   });
+  time("stream read, then RMW 64-B blocks", [&](int r) {
+    readall<<<grid, 256>>>((const u4v *)d[r & 1], bytes / 16, sink);
+    rmw_block<64, false><<<grid, 256>>>(d[r & 1], stride, n, 16, v);
+  });
+  time("stream read, then RMW 64-B blocks, nt", [&](int r) {
+    readall<<<grid, 256>>>((const u4v *)d[r & 1], bytes / 16, sink);
+    rmw_block<64, true><<<grid, 256>>>(d[r & 1], stride, n, 16, v);
+  });
+  time("stream read, then RMW 128-B lines", [&](int r) {
+    readall<<<grid, 256>>>((const u4v *)d[r & 1], bytes / 16, sink);
+    rmw_block<128, false><<<grid, 256>>>(d[r & 1], stride, n, 16, v);
+  });
+  time("RMW 64-B blocks only", [&](int r) { rmw_block<64, false><<<grid, 256>>>(d[r & 1], stride, n, 16, v); });
   return 0;
 }
