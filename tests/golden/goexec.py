@@ -23,6 +23,12 @@ Struct values are shared, not copied, on assignment: the code the path executes 
 copies a struct and then changes both copies. Values from outside the loaded packages
 (a `*testing.T`, a link endpoint, `log.Printf`) are Python stubs the caller supplies.
 
+For cgo code (this repo's own Go shim, bindings/go/checksum, run by
+tests/test_go_shim_exec.py): package-level `var`s (initialised on first use), `switch`,
+`make([]T, n)` for non-byte T, multi-value assignment, `&s[i]` as a reference into the
+slice, and `(*T)(x)` conversions; `C.*` names and `unsafe.Pointer` are stubs the caller
+supplies (the test binds them to the C ABI through ctypes).
+
 Function bodies are parsed lazily, when first called, so code the path does not reach
 (options parsing, the TCP state machine, ...) is only skipped over.
 tests/golden/make_refexec.py uses it to produce known-answer vectors "from the
@@ -39,6 +45,9 @@ import re
 WIDTH = {"uint8": 8, "byte": 8, "uint16": 16, "uint32": 32, "uint64": 64, "uint": 64,
          "int8": 8, "int16": 16, "int32": 32, "int64": 64, "int": 64}
 SIGNED = {"int8", "int16", "int32", "int64", "int"}
+# named integer types (`type Mode int`) -> their underlying type: an Int keeps the
+# named type (methods dispatch on it) and wraps at the underlying width
+NAMED_INT = {}
 
 
 class GoPanic(Exception):
@@ -62,6 +71,7 @@ class Int:
 def wrap(v, t):
     if t == "untyped":
         return v
+    t = NAMED_INT.get(t, t)
     w = WIDTH[t]
     v &= (1 << w) - 1
     if t in SIGNED and v >= 1 << (w - 1):
@@ -138,6 +148,14 @@ class GoList:
     def set(self, i, x):
         self.get(i)
         self.items[i] = x
+
+
+class Ref:
+    """`&s[i]`: element i of a slice (the start of the memory a cgo call is handed)."""
+    __slots__ = ("s", "i")
+
+    def __init__(self, s, i):
+        self.s, self.i = s, i
 
 
 class Closure:
@@ -506,6 +524,37 @@ class Parser:
                     cond = s[1]
             self.nolit = False
             return ("for", init, cond, post, self.block())
+        if v == "switch":  # switch [init;] [tag] { case a, b: ... default: ... }
+            self.next()
+            init = tag = None
+            self.nolit = True
+            if self.val() != "{":
+                s = self.simple()
+                if self.accept(";"):
+                    init = s
+                    s = None if self.val() == "{" else self.simple()
+                tag = s[1] if s else None
+            self.nolit = False
+            self.expect("{")
+            clauses = []
+            while not self.accept("}"):
+                if self.accept(";"):
+                    continue
+                if self.accept("default"):
+                    conds = None
+                else:
+                    self.expect("case")
+                    conds = [self.expr()]
+                    while self.accept(","):
+                        conds.append(self.expr())
+                self.expect(":")
+                body = []
+                while self.val() not in ("case", "default", "}"):
+                    if self.accept(";"):
+                        continue
+                    body.append(self.stmt())
+                clauses.append((conds, body))
+            return ("switch", init, tag, clauses)
         if v == "var":
             self.next()
             name = self.next()[1]
@@ -531,6 +580,7 @@ class Package:
         self.name = name
         self.funcs, self.methods, self.consts, self.types, self.imports = {}, {}, {}, {}, {}
         self.structs = {}  # name -> [(field, type)]
+        self.vars = {}  # package-level var: name -> [type, init expr, done, value]
 
 
 class Return(Exception):
@@ -602,16 +652,32 @@ class Interp:
                     p.skip_balanced()
                 else:
                     pkg.types[tname] = p.parse_type()
+                    if pkg.types[tname] in WIDTH:
+                        NAMED_INT[tname] = pkg.types[tname]
             elif v == "var":
                 p.next()
-                if p.val() == "(":
-                    p.skip_balanced()
-                else:
-                    while p.val() != ";":
-                        if p.val() in "([{":
-                            p.skip_balanced()
-                        else:
-                            p.next()
+                at = p.i
+                try:
+                    specs = []
+                    if p.accept("("):
+                        while not p.accept(")"):
+                            if p.accept(";"):
+                                continue
+                            specs.append(self._var_spec(p))
+                    else:
+                        specs.append(self._var_spec(p))
+                    for nm, t, e in specs:
+                        pkg.vars[nm] = [t, e, False, None]
+                except (SyntaxError, IndexError, KeyError, ValueError):
+                    p.i = at  # not in the subset: skipped, as it is never used on the path
+                    if p.val() == "(":
+                        p.skip_balanced()
+                    else:
+                        while p.val() != ";":
+                            if p.val() in "([{":
+                                p.skip_balanced()
+                            else:
+                                p.next()
             elif v == "func":
                 p.next()
                 recv = None
@@ -637,6 +703,23 @@ class Interp:
                 raise SyntaxError(f"{path}: unexpected top-level {v!r}")
         pkg.imports.update(imports)
         return pkg
+
+    @staticmethod
+    def _var_spec(p):
+        nm = p.next()[1]
+        t = p.parse_type() if p.val() not in ("=", ";", ")") else None
+        e = p.expr() if p.accept("=") else None
+        if p.val() not in (";", ")"):
+            raise SyntaxError("var spec")
+        return nm, t, e
+
+    def _var(self, pkg, n):
+        slot = pkg.vars[n]
+        if not slot[2]:
+            t, e = slot[0], slot[1]
+            v = self._eval(e, [{}], pkg) if e is not None else self._zero(t, pkg)
+            slot[2], slot[3] = True, self._convert(v, t, pkg) if t else v
+        return slot[3]
 
     def _consts(self, p, pkg):
         specs = []
@@ -741,9 +824,12 @@ class Interp:
         elif k == "assign":
             _, op, lhs, rhs = s
             vals = [self._eval(e, env, pkg) for e in rhs]
+            if len(lhs) > 1 and len(vals) == 1 and isinstance(vals[0], tuple):  # a, b := f()
+                vals = list(vals[0])
             for target, v in zip(lhs, vals):
                 if op == ":=":
-                    env[-1][target[1]] = v
+                    if target[1] != "_":
+                        env[-1][target[1]] = v
                     continue
                 if op != "=":
                     v = self._binop(op[:-1], self._eval(target, env, pkg), v)
@@ -792,6 +878,30 @@ class Interp:
                     env.pop()
         elif k == "block":
             self._exec_block(s[1], env, pkg)
+        elif k == "switch":
+            _, init, tag, clauses = s
+            env.append({})
+            try:
+                if init:
+                    self._exec(init, env, pkg)
+                tv = self._eval(tag, env, pkg) if tag is not None else True
+                chosen = None
+                for conds, body in clauses:
+                    if conds is None:
+                        continue
+                    for c in conds:
+                        cv = self._eval(c, env, pkg)
+                        if (cv is True and tag is None) or (tag is not None and self._binop("==", tv, cv)):
+                            chosen = body
+                            break
+                    if chosen is not None:
+                        break
+                if chosen is None:
+                    chosen = next((b for c, b in clauses if c is None), None)
+                if chosen is not None:
+                    self._exec_block(chosen, env, pkg)
+            finally:
+                env.pop()
         else:
             raise NotImplementedError(k)
 
@@ -802,6 +912,8 @@ class Interp:
             scope[target[1]] = self._convert(v, old.t, pkg) if isinstance(old, Int) else v
         elif target[0] == "index":
             base = self._eval(target[1], env, pkg)
+            if isinstance(base, GoList) and isinstance(v, Int) and base.t.startswith("[]"):
+                v = self._convert(v, base.t[2:], pkg)  # the element type's width
             base.set(self._int(self._eval(target[2], env, pkg)), v if isinstance(base, GoList) else v.v)
         elif target[0] == "sel":
             st = self._eval(target[1], env, pkg)
@@ -874,7 +986,7 @@ class Interp:
         t = self._resolve_type(t, pkg)
         u = self._underlying(t, pkg)
         if u in WIDTH:
-            return Int(v.v if isinstance(v, Int) else int(v), u)
+            return Int(v.v if isinstance(v, Int) else int(v), t if t in NAMED_INT else u)
         if u == "[]byte" or u == "[]uint8":
             if isinstance(v, Str):
                 return from_bytes(v.b, t if t != u else "[]byte")
@@ -947,6 +1059,8 @@ class Interp:
                 return None
             if n in pkg.consts:
                 return self._const(pkg, n)
+            if n in pkg.vars:
+                return self._var(pkg, n)
             raise NameError(n)
         if k == "bin":
             op = e[1]
@@ -956,6 +1070,12 @@ class Interp:
                 return bool(self._eval(e[2], env, pkg)) or bool(self._eval(e[3], env, pkg))
             return self._binop(op, self._eval(e[2], env, pkg), self._eval(e[3], env, pkg))
         if k == "un":
+            if e[1] == "&" and e[2][0] == "index":  # &s[i]: a reference into the slice
+                base = self._eval(e[2][1], env, pkg)
+                if isinstance(base, (Slice, GoList)):
+                    i = self._int(self._eval(e[2][2], env, pkg))
+                    base.get(i)  # bounds check, as Go's
+                    return Ref(base, i)
             x = self._eval(e[2], env, pkg)
             if e[1] in ("&", "*"):  # pointers: the value itself (shared, see module doc)
                 return x
@@ -1004,6 +1124,9 @@ class Interp:
                 other = self.pkgs.get(pkg.imports[base[1]])
                 if other is not None and e[2] in other.consts:
                     return self._const(other, e[2])
+                stub = self.stubs.get(f"{pkg.imports[base[1]]}.{e[2]}")
+                if stub is not None and not callable(stub):  # a stub constant (C.YU_OK)
+                    return stub
                 raise NameError(f"{base[1]}.{e[2]}")
             st = self._eval(base, env, pkg)
             if isinstance(st, Struct):
@@ -1053,7 +1176,10 @@ class Interp:
                 if n == "make":
                     t = args[0][1]
                     size = self._int(self._eval(args[1], env, pkg))
-                    return Slice(bytearray(size), 0, size, size, t)
+                    if t in ("[]byte", "[]uint8") or self._underlying(t, pkg) in ("[]byte", "[]uint8"):
+                        return Slice(bytearray(size), 0, size, size, t)
+                    et = t[2:]
+                    return GoList([Int(0, et) if et in WIDTH else None for _ in range(size)], t)
                 if n == "copy":
                     dst, src = self._eval(args[0], env, pkg), self._eval(args[1], env, pkg)
                     b = src.bytes() if isinstance(src, Slice) else src.b
@@ -1115,6 +1241,8 @@ class Interp:
                 if fn is not None:
                     return self._invoke(fn, recv, vals)
             raise NameError(f"method {recv.t}.{name}")
+        if fexpr[0] == "un" and fexpr[1] == "*" and len(args) == 1:  # (*T)(x): a pointer conversion
+            return self._eval(args[0], env, pkg)
         raise NotImplementedError(fexpr)
 
 

@@ -365,8 +365,11 @@ YU_MODE_COUNT = 10
 def test_host_staging_pool_bound_and_setting():
     """The host path's context pool (include/yucsum.h, Host-path staging): K from
     YU_HOST_CONTEXTS (default 4, clamped to 1..64, read without the tuning gate), no
-    staging before a first call, the per-context bounds as the header states them."""
+    staging before a first call (or after a trim), the per-context bounds as the header
+    states them."""
     L = _lib.lib()
+    if L.yu_device_count() > 0:  # (on a GPU box earlier tests of this process may hold staging)
+        assert L.yu_host_staging_trim(0) == 0
     assert L.yu_host_staging_bytes(0, None) == 0 and L.yu_host_staging_bytes(-1, None) == 0
     assert L.yu_host_staging_trim(64) == _lib.YU_ENODEV
     src = open(HEADER).read()
@@ -382,3 +385,26 @@ def test_host_staging_pool_bound_and_setting():
         r = subprocess.run([__import__("sys").executable, "-c", probe], env=env, capture_output=True, text=True,
                            timeout=60)
         assert r.returncode == 0 and int(r.stdout) == want, (val, r.stdout, r.stderr)
+
+
+_ORDER = r"""
+import sys
+sys.path.insert(0, %r)
+from yustack_amd import _lib
+n = _lib.lib().yu_device_count()
+import torch
+print(n, torch.cuda.is_available())
+"""
+
+
+@pytest.mark.gpu
+def test_library_first_then_torch_share_the_device():
+    """PyTorch-ROCm bundles its own HIP runtime; the library binds /opt/rocm's. When the
+    library initialised its runtime first, torch's saw no device (and the other way
+    round: profiles/r05/load_order_r05.log). The loader now brings torch's in first, so
+    a process that calls the library before touching torch still has both."""
+    r = subprocess.run([__import__("sys").executable, "-c", _ORDER % ROOT], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n, ok = r.stdout.split()
+    assert int(n) >= 1 and ok == "True", r.stdout

@@ -1,13 +1,17 @@
-"""The Go shim's own Go code, executed. bindings/go/checksum/checksum.go keeps the
-reference's three signatures (checksum/checksum.go:4-35) and sums buffers under
-256 bytes in Go (goSum), calling the C ABI only above that. There is no Go toolchain
-here, so the file runs in tests/golden/goexec.py (the Go-subset interpreter the
-fixture generator runs the reference's source with): every call below stays on the
-pure-Go path and is compared with the oracle (oracle/oracle.py, checksum.go:4-35
-restated). Parity unpinned by a real Go build; this pins the shim's Go-side logic
-(odd tails, the uint32 accumulation, the combine, the pseudo header) against the
-same oracle the GPU path is held to."""
+"""The Go shim's own Go code, executed. bindings/go/checksum keeps the reference's
+three signatures (checksum/checksum.go:4-35), sums buffers under 256 bytes in Go
+(goSum) and calls the C ABI for longer ones and for batches (batch.go). There is no Go
+toolchain here, so the files run in tests/golden/goexec.py (the Go-subset interpreter
+the fixture generator runs the reference's source with), with every `C.*` name bound
+to libyucsum through ctypes: the shim's conversions, argument checks and status
+mapping run as written, and its C calls reach the product library. Results are compared
+with the oracle (oracle/oracle.py, checksum.go:4-35 and the senders restated).
+Parity unpinned by a real Go build; this pins the shim's Go-side logic against the
+same oracle the GPU path is held to. The batched calls need a GPU (`-m gpu` below);
+without one the shim must map the library's YU_ENODEV to its ErrNoDevice."""
+import ctypes
 import os
+import re
 import sys
 
 import numpy as np
@@ -20,11 +24,101 @@ import goexec as G  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
+class GoError:
+    """An `error` value made by the errors.New / fmt.Errorf stubs."""
+
+    def __init__(self, msg):
+        self.msg = msg
+
+    def __repr__(self):
+        return f"error({self.msg!r})"
+
+
+_CTYPES = {"uint8": np.uint8, "uint16": np.uint16, "uint32": np.uint32, "uint64": np.uint64,
+           "int": np.int64, "int32": np.int32, "C.int": np.int32, "C.uint16_t": np.uint16,
+           "C.uint64_t": np.uint64}
+
+
+def _marshal(ref, keep, post):
+    """A `&s[i]` handed to C: bytes in place (the slice's bytearray), other element
+    types copied into a numpy array and, after the call, back into the Go slice."""
+    s = ref.s
+    if isinstance(s, G.Slice):
+        cbuf = (ctypes.c_char * len(s.buf)).from_buffer(s.buf)
+        keep.append(cbuf)
+        return ctypes.addressof(cbuf) + s.off + ref.i
+    et = s.t[2:]
+    arr = np.array([x.v for x in s.items], dtype=_CTYPES[et])
+    keep.append(arr)
+
+    def back():
+        for k in range(len(s.items)):
+            s.items[k] = G.Int(int(arr[k]), s.items[k].t)
+    post.append(back)
+    return arr.ctypes.data + ref.i * arr.itemsize
+
+
+def cgo_stubs():
+    """The `C.*`, `unsafe`, `errors` and `fmt` names the shim uses: C types as integer
+    conversions, C functions as ctypes calls into libyucsum, C constants from yucsum.h."""
+    from yustack_amd import _lib
+    L = _lib.lib()
+
+    def cfunc(name):
+        f = getattr(L, name)
+
+        def call(*args):
+            keep, post, cargs = [], [], []
+            for a in args:
+                if isinstance(a, G.Ref):
+                    cargs.append(_marshal(a, keep, post))
+                elif isinstance(a, G.Int):
+                    cargs.append(a.v)
+                else:
+                    cargs.append(a)
+            r = f(*cargs)
+            for fn in post:
+                fn()
+            return G.Int(r, "int32") if isinstance(r, int) else r
+        return call
+
+    stubs = {"errors.New": lambda m: GoError(m.b.decode()),
+             "fmt.Errorf": lambda f, *a: GoError(f.b.decode()),
+             "unsafe.Pointer": lambda x: x,
+             "C.GoString": lambda b: G.Str(b or b"")}
+    for t, w in (("C.int", "int32"), ("C.uint64_t", "uint64"), ("C.uint32_t", "uint32"),
+                 ("C.uint16_t", "uint16"), ("C.size_t", "uint64")):
+        stubs[t] = (lambda w: lambda x: G.Int(x.v, w))(w)
+    for name in _lib.EXPORTS:
+        stubs["C." + name] = cfunc(name)
+    hdr = open(os.path.join(ROOT, "include", "yucsum.h")).read()
+    for nm, v in re.findall(r"#define (YU_\w+) \(?(-?(?:0x[0-9A-Fa-f]+|\d+))u?\)?\s", hdr):
+        stubs["C." + nm] = G.Int(int(v, 0))
+    stubs["C.YU_HOST_CONTEXT_PINNED_MAX"] = G.Int(_lib.HOST_CONTEXT_PINNED_MAX)
+    stubs["C.YU_HOST_BURST_CONTEXT_PINNED_MAX"] = G.Int(_lib.HOST_BURST_CONTEXT_PINNED_MAX)
+    return stubs
+
+
+class FakeT:
+    """A *testing.T for the shim's own Go tests: Fatal / Fatalf end the test."""
+
+    def Fatal(self, *a):
+        raise G.GoFatal(repr(a))
+
+    def Fatalf(self, *a):
+        raise G.GoFatal(repr(a))
+
+
+def load_shim():
+    it = G.Interp(os.path.join(ROOT, "bindings", "go"))
+    it.stubs.update(cgo_stubs())
+    it.load("checksum", files=["checksum.go", "batch.go", "checksum_test.go"])
+    return it
+
+
 @pytest.fixture(scope="module")
 def shim():
-    it = G.Interp(os.path.join(ROOT, "bindings", "go"))
-    it.load("checksum", files=["checksum.go"])
-    return it
+    return load_shim()
 
 
 def test_checksum_short_buffers(shim):
@@ -60,3 +154,72 @@ def test_pseudo_header_checksum(shim):
         proto = (6, 17, 1, 0, 255)[k % 5]
         got = shim.call("checksum", "PseudoHeaderChecksum", G.Int(proto, "uint32"), G.Str(src), G.Str(dst)).v
         assert got == O.pseudo_header_checksum(proto, src, dst), (proto, src, dst)
+
+
+def test_checksum_long_buffers_through_the_c_abi(shim):
+    """Buffers of 256 bytes and more go through `C.yu_checksum` (the product's scalar
+    drop-in) with the shim's pointer and size conversions; every result equals the
+    oracle's, including the uint32 wrap past 131072 bytes."""
+    rng = np.random.default_rng(5)
+    for n in list(range(256, 300)) + [1499, 1500, 4096, 65535, 131072, 131073, 200001]:
+        b = bytes(rng.integers(0, 256, size=n, dtype=np.uint8))
+        i = int(rng.integers(0, 65536))
+        assert shim.call("checksum", "Checksum", G.from_bytes(b), G.Int(i, "uint16")).v == O.checksum(b, i), n
+    ff = b"\xff" * 131074
+    assert shim.call("checksum", "Checksum", G.from_bytes(ff), G.Int(0xFFFF, "uint16")).v == 65534
+
+
+def test_shim_go_tests(shim):
+    """The shim's own Go tests that need no GPU and no goroutines: TestRFC1071 and
+    TestShortArgumentsRejected (too-short side arrays, a wrapping size product and a
+    length past the data are errors before any C call)."""
+    for name in ("TestRFC1071", "TestShortArgumentsRejected"):
+        shim.call("checksum", name, FakeT())
+
+
+def test_batch_without_a_device_is_err_no_device(shim):
+    """Valid batched calls reach the C ABI; with no HIP device it returns YU_ENODEV and
+    the shim's status() maps it to the package's ErrNoDevice."""
+    from yustack_amd import _lib
+    if _lib.lib().yu_device_count() > 0:
+        pytest.skip("a HIP device is visible (the GPU test below covers this path)")
+    data = G.from_bytes(bytes(4 * 100))
+    out = G.GoList([G.Int(0, "uint16")] * 4, "[]uint16")
+    err = shim.call("checksum", "BatchHostUniform", data, G.Int(100, "uint64"), G.Int(100, "uint32"),
+                    G.Int(4, "uint64"), G.Int(0, "Mode"), None, None, out, G.Int(0, "int"))
+    assert err is shim.pkgs["checksum"].vars["ErrNoDevice"][3]
+    assert shim.call("checksum", "HostContexts").v >= 1
+
+
+@pytest.mark.gpu
+def test_batch_calls_on_the_gpu(dev, oracle_c):
+    """BatchHostUniform (sendTCP field values, address records) and BatchHostRagged
+    (RAW with initial values, one shard and two) run through the interpreted shim into
+    libyucsum on the GPU; the results it hands back in `out` equal the oracle's."""
+    it = load_shim()
+    rng = np.random.default_rng(21)
+    n, L = 300, 1500
+    data = rng.integers(0, 256, size=n * L, dtype=np.uint8)
+    data.reshape(n, L)[:, 12] = 0x50
+    addrs = rng.integers(0, 256, size=8 * n, dtype=np.uint8)
+    want = oracle_c.batch(data, O.MODE_TCP, stride=L, length=L, n=n, addrs=addrs)
+    out = G.GoList([G.Int(0, "uint16") for _ in range(n)], "[]uint16")
+    err = it.call("checksum", "BatchHostUniform", G.from_bytes(data.tobytes()), G.Int(L, "uint64"),
+                  G.Int(L, "uint32"), G.Int(n, "uint64"), G.Int(2, "Mode"), None,
+                  G.from_bytes(addrs.tobytes()), out, G.Int(0, "int"))
+    assert err is None, err
+    assert [x.v for x in out.items] == [int(v) for v in want]
+
+    lens = rng.integers(40, 1501, size=n)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    rag = rng.integers(0, 256, size=int(offs[-1]), dtype=np.uint8)
+    init = rng.integers(0, 65536, size=n, dtype=np.uint16)
+    want = oracle_c.batch(rag, O.MODE_RAW, offsets=offs, initial_arr=init)
+    for devices in ([], [G.Int(0, "int"), G.Int(0, "int")]):
+        out = G.GoList([G.Int(0, "uint16") for _ in range(n)], "[]uint16")
+        err = it.call("checksum", "BatchHostRagged", G.from_bytes(rag.tobytes()),
+                      G.GoList([G.Int(int(o), "uint64") for o in offs], "[]uint64"), G.Int(0, "Mode"),
+                      G.GoList([G.Int(int(v), "uint16") for v in init], "[]uint16"), None, out, *devices)
+        assert err is None, err
+        assert [x.v for x in out.items] == [int(v) for v in want], len(devices)

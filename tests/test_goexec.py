@@ -16,7 +16,9 @@ package demo
 
 import (
 	"encoding/binary"
+	"errors"
 	"log"
+	"unsafe"
 )
 
 type Counter struct {
@@ -87,7 +89,70 @@ func NilLen(b []byte) int {
 func Third() int {
 	return third
 }
+
+type Kind int
+
+func (k Kind) Double() int {
+	return int(k) * 2
+}
+
+var table = []int{5, 7, 9}
+
+var errShort = errors.New("short")
+
+func Classify(x int) string {
+	switch {
+	case x < 0:
+		return "neg"
+	case x == 0, x == 100:
+		return "edge"
+	default:
+		return "pos"
+	}
+}
+
+func Tag(k Kind) int {
+	switch k {
+	case 1, 2:
+		return 10
+	case 3:
+		return 30
+	}
+	return -1
+}
+
+func Pair(a, b int) (int, int) {
+	return b, a
+}
+
+func Swap(a, b int) int {
+	x, y := Pair(a, b)
+	return x*10 + y
+}
+
+func Words(n int) int {
+	w := make([]uint16, n)
+	w[n-1] = 65535
+	w[n-1]++
+	return len(w) + int(w[n-1]) + table[2]
+}
+
+func Check(b []byte) error {
+	if len(b) < 2 {
+		return errShort
+	}
+	return nil
+}
+
+func Addr(b []byte) *uint8 {
+	return (*uint8)(unsafe.Pointer(&b[1]))
+}
 '''
+
+
+class _Err:
+    def __init__(self, m):
+        self.m = m
 
 
 @pytest.fixture(scope="module")
@@ -96,6 +161,7 @@ def it(tmp_path_factory):
     d.mkdir()
     (d / "demo.go").write_text(SRC)
     i = G.Interp(str(d.parent))
+    i.stubs.update({"errors.New": lambda m: _Err(m.b), "unsafe.Pointer": lambda x: x})
     i.load("demo")
     return i
 
@@ -126,3 +192,31 @@ def test_typed_wrap_slices_and_binary(it):
 def test_bounds_panic(it):
     with pytest.raises(G.GoPanic):
         it.call("demo", "Cut", G.from_bytes(b"ab"))
+
+
+def test_switch_vars_named_types_multi_assign(it):
+    """cgo-shim constructs: tagless and tagged switch, package-level vars (initialised
+    on first use), methods on a named integer type, multi-value assignment and
+    `make([]uint16, n)` with uint16 wrap."""
+    assert [it.call("demo", "Classify", G.Int(x, "int")).b for x in (-3, 0, 100, 5)] == \
+        [b"neg", b"edge", b"edge", b"pos"]
+    assert [it.call("demo", "Tag", G.Int(k, "Kind")).v for k in (1, 2, 3, 4)] == [10, 10, 30, -1]
+    k = it.call("demo", "Tag", G.Int(3, "Kind"))
+    assert k.v == 30
+    assert it.method("demo", G.Int(21, "Kind"), "Double").v == 42
+    assert it.call("demo", "Swap", G.Int(1, "int"), G.Int(2, "int")).v == 21
+    assert it.call("demo", "Words", G.Int(3, "int")).v == 3 + 0 + 9
+    e = it.call("demo", "Check", G.from_bytes(b"a"))
+    assert isinstance(e, _Err) and e is it.call("demo", "Check", G.from_bytes(b""))  # one var, one value
+    assert it.call("demo", "Check", G.from_bytes(b"ab")) is None
+
+
+def test_element_reference_and_pointer_conversion(it):
+    """`&b[1]` is a reference into the slice (what a cgo call is handed), passed through
+    `unsafe.Pointer` and a `(*T)(x)` conversion unchanged; `&b[1]` of a 1-byte slice
+    panics, as Go's bounds check does."""
+    b = G.from_bytes(b"xyz")
+    r = it.call("demo", "Addr", b)
+    assert isinstance(r, G.Ref) and r.s.buf is b.buf and r.i == 1 and r.s.get(r.i).v == ord("y")
+    with pytest.raises(G.GoPanic):
+        it.call("demo", "Addr", G.from_bytes(b"x"))

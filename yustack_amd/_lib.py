@@ -58,6 +58,15 @@ def lib() -> ctypes.CDLL:
         raise ImportError(
             f"{LIB_PATH} not built — run `python -c 'import __graft_entry__ as g; g.build()'` "
             "or `make -C yustack_amd/csrc`")
+    # One process, two HIP runtimes: PyTorch-ROCm bundles its own libamdhip64 (no
+    # SONAME), the library binds /opt/rocm's. Measured on the GPU box
+    # (tools/load_order_probe.py): with torch's loaded first both see the device in
+    # either order of first use; with this library loaded first, whichever runtime
+    # initialises second sees no device. So torch, when installed, is loaded first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     c = ctypes
     vp, u8, u16, u32, u64, sz, i32 = (c.c_void_p, c.c_uint8, c.c_uint16, c.c_uint32,
