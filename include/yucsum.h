@@ -449,6 +449,13 @@ int yu_abi_version(void);
 const char *yu_strerror(int status);
 /* Number of HIP devices (0 when none / no driver). Never fails. */
 int yu_device_count(void);
+/* Path of the HIP runtime (libamdhip64) this library's HIP calls are bound
+ * to, as the dynamic loader resolved them (dladdr of the library's own
+ * reference to hipGetDevice); NULL if it cannot be told. No device needed.
+ * A process with two HIP runtimes (PyTorch-ROCm bundles one) must have this
+ * library bound to the runtime the rest of the process uses: the Python
+ * loader checks it ("One HIP runtime per process"). */
+const char *yu_hip_runtime_path(void);
 /* Name of the kernel variant the uniform path would launch for this shape
  * (for profiling and tests; no device needed). Returns a static string. */
 const char *yu_uniform_variant(uint64_t stride, uint32_t len, int mode,

@@ -408,3 +408,48 @@ def test_library_first_then_torch_share_the_device():
     assert r.returncode == 0, r.stderr[-2000:]
     n, ok = r.stdout.split()
     assert int(n) >= 1 and ok == "True", r.stdout
+
+
+_MISORDERED = r"""
+import ctypes, sys
+sys.path.insert(0, %r)
+ctypes.CDLL(%r)          # a user program loads the library by ctypes first ...
+import torch             # ... and torch (with its own HIP runtime) after it
+from yustack_amd import _lib
+try:
+    _lib.lib()
+except ImportError as e:
+    print("refused:", e)
+    sys.exit(0)
+print("loaded", _lib.lib().yu_hip_runtime_path())
+sys.exit(3)
+"""
+
+_ORDERED = r"""
+import sys
+sys.path.insert(0, %r)
+from yustack_amd import _lib
+L = _lib.lib()
+import os
+print(os.path.realpath(L.yu_hip_runtime_path().decode()), os.path.realpath(_lib.torch_hip_runtime() or ""))
+"""
+
+
+def test_runtime_binding_is_checked_at_load():
+    """the loader checks which HIP runtime the library's calls are
+    bound to (yu_hip_runtime_path, dladdr of its own hipGetDevice reference). Through
+    the loader (torch first) it is torch's bundled runtime; a library loaded by ctypes
+    before torch is bound to /opt/rocm's, and the loader refuses it with an ImportError
+    that names the fix, instead of a later silent "no device". No GPU needed: binding
+    happens at load time."""
+    import sys
+    r = subprocess.run([sys.executable, "-c", _ORDERED % ROOT], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    ours, theirs = r.stdout.split()
+    if theirs == os.path.realpath(""):  # a torch that uses the system runtime: nothing to check
+        pytest.skip("torch bundles no HIP runtime here")
+    assert ours == theirs
+    r = subprocess.run([sys.executable, "-c", _MISORDERED % (ROOT, _lib.LIB_PATH)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, (r.stdout, r.stderr[-2000:])
+    assert "refused:" in r.stdout and "import torch" in r.stdout and "/opt/rocm" in r.stdout, r.stdout

@@ -173,3 +173,71 @@ def test_bursts_do_not_wait_behind_bulk_batches(dev, oracle_c):
           f"a bulk call {typical_bulk * 1e3:.1f} ms")
     assert len(bulk_times) >= 6
     assert lat[-1] < typical_bulk / 2, (lat[-1], typical_bulk)
+
+
+_FAILED_RESERVE = r"""
+import sys
+sys.path.insert(0, %r)
+import numpy as np
+from yustack_amd import _lib, batch
+from oracle import oracle as O
+rng = np.random.default_rng(11)
+n = 30000  # 45 MB pageable: the pipelined (bulk) path, 3 slots of 32 MiB
+b = rng.integers(0, 256, size=n * 1500, dtype=np.uint8)
+want = O.C().batch(b, O.MODE_RAW, stride=1500, length=1500, n=n, threads=8)
+try:
+    batch.checksum_host_uniform(b, 1500, 1500, n, "raw")
+    raise SystemExit("the injected allocation failure was not reported")
+except _lib.YuError as e:
+    assert e.status == _lib.YU_ENOMEM, e
+# the failed reserve freed what it had allocated: nothing is held
+assert _lib.host_staging(0) == (0, 0), _lib.host_staging(0)
+# the next call (the injection fires once) reserves afresh and is bit-exact
+assert np.array_equal(batch.checksum_host_uniform(b, 1500, 1500, n, "raw"), want)
+p, d = _lib.host_staging(0)
+assert 0 < p <= _lib.HOST_CONTEXT_PINNED_MAX and 0 < d <= _lib.HOST_CONTEXT_DEVICE_MAX, (p, d)
+print("ok", p, d)
+"""
+
+
+@pytest.mark.parametrize("fail_at", [1, 6, 27])
+def test_failed_reserve_holds_no_staging(dev, fail_at):
+    """a staging allocation that fails midway (the fault-injection knob
+    YU_HOST_FAIL_ALLOC=k under YU_TUNING=1 fails the k-th one: the first pinned buffer,
+    one in slot 0, one in slot 2) frees everything the reserve had allocated, so the
+    pool holds nothing after the ENOMEM, and the next call reserves afresh and is
+    bit-exact."""
+    env = dict(os.environ, YU_TUNING="1", YU_HOST_FAIL_ALLOC=str(fail_at), YU_HOST_CONTEXTS="1")
+    r = subprocess.run([sys.executable, "-c", _FAILED_RESERVE % ROOT], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert r.stdout.startswith("ok")
+
+
+def test_trim_from_a_thread_that_never_called_the_library(dev, oracle_c):
+    """a trim from a fresh thread (whose current device was never
+    set by the library) frees the contexts with each context's own device current and
+    restores the thread's device; the next host call on another thread is bit-exact."""
+    import torch
+    rng = np.random.default_rng(12)
+    b, a = _tcp_batch(rng, 20000)
+    want = oracle_c.batch(b, O.MODE_TCP, stride=1500, length=1500, n=20000, addrs=a, threads=8)
+    assert np.array_equal(batch.checksum_host_uniform(b, 1500, 1500, 20000, "tcp", addrs=a), want)
+    assert _lib.host_staging(0)[0] > 0
+    out = {}
+
+    def trim():
+        out["rc"] = _lib.lib().yu_host_staging_trim(0)
+        out["dev"] = torch.cuda.current_device()
+
+    t = threading.Thread(target=trim)
+    t.start()
+    t.join(timeout=60)
+    assert out == {"rc": 0, "dev": 0}, out
+    assert _lib.host_staging(0) == (0, 0)
+    got = {}
+    t = threading.Thread(target=lambda: got.update(v=batch.checksum_host_uniform(b, 1500, 1500, 20000, "tcp",
+                                                                                  addrs=a)))
+    t.start()
+    t.join(timeout=60)
+    assert np.array_equal(got["v"], want)

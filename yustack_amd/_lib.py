@@ -23,7 +23,7 @@ EXPORTS = (
     "yu_csum_fill_host_uniform", "yu_csum_fill_host_ragged", "yu_csum_fill_host_iov",
     "yu_abi_version", "yu_strerror", "yu_device_count", "yu_uniform_variant", "yu_uniform_variant_n",
     "yu_ragged_variant", "yu_ragged_variant_n", "yu_ragged_fill_variant_n",
-    "yu_host_contexts", "yu_host_staging_bytes", "yu_host_staging_trim",
+    "yu_host_contexts", "yu_host_staging_bytes", "yu_host_staging_trim", "yu_hip_runtime_path",
 )
 
 # Host-path staging bounds (include/yucsum.h): per context, between calls.
@@ -62,13 +62,18 @@ def lib() -> ctypes.CDLL:
     # SONAME), the library binds /opt/rocm's. Measured on the GPU box
     # (tools/load_order_probe.py): with torch's loaded first both see the device in
     # either order of first use; with this library loaded first, whichever runtime
-    # initialises second sees no device. So torch, when installed, is loaded first.
+    # initialises second sees no device. So torch, when installed, is loaded first
+    # (a torch that fails to import for any reason is skipped: the library itself
+    # does not need it), and the binding is then checked (check_runtime).
     try:
         import torch  # noqa: F401
-    except ImportError:
+    except Exception:  # noqa: BLE001 — any broken torch install: load without it
         pass
     L = ctypes.CDLL(LIB_PATH)
     c = ctypes
+    L.yu_hip_runtime_path.restype = c.c_char_p
+    L.yu_hip_runtime_path.argtypes = []
+    check_runtime(L)
     vp, u8, u16, u32, u64, sz, i32 = (c.c_void_p, c.c_uint8, c.c_uint16, c.c_uint32,
                                       c.c_uint64, c.c_size_t, c.c_int)
     L.yu_checksum.restype = u16
@@ -128,6 +133,46 @@ def lib() -> ctypes.CDLL:
     del u8
     _lib = L
     return L
+
+
+def torch_hip_runtime() -> str | None:
+    """Path of the HIP runtime PyTorch-ROCm bundles (torch/lib/libamdhip64*), when
+    torch is imported and that file is mapped into this process; else None (no
+    torch, or a torch that uses the system runtime like this library)."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is None or not getattr(torch, "__file__", None):
+        return None
+    tlib = os.path.join(os.path.dirname(os.path.realpath(torch.__file__)), "lib") + os.sep
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                path = line.split(maxsplit=5)[-1].strip()
+                if path.startswith(tlib) and os.path.basename(path).startswith("libamdhip64"):
+                    return path
+    except OSError:  # pragma: no cover - /proc is always there on Linux
+        return None
+    return None
+
+
+def check_runtime(L) -> None:
+    """One HIP runtime per process: when torch's bundled runtime is
+    loaded, the library's HIP calls must be bound to it. They are not when the
+    library was loaded (e.g. by ctypes) before torch was imported; every HIP call of
+    the library would then run on a second runtime, and whichever of the two
+    initialises second sees no device (profiles/r05/load_order_r05.log). Raises
+    ImportError naming the fix instead of failing later as "no device"."""
+    theirs = torch_hip_runtime()
+    if theirs is None:
+        return
+    raw = L.yu_hip_runtime_path()
+    ours = raw.decode() if raw else None
+    if ours is None or os.path.realpath(ours) != os.path.realpath(theirs):
+        raise ImportError(
+            f"{LIB_PATH} is bound to the HIP runtime {ours}, but torch uses {theirs}: two HIP "
+            "runtimes in one process (the one initialised second sees no device). The library "
+            "was loaded before torch; import torch (or yustack_amd) before loading "
+            "libyucsum.so by any other means.")
 
 
 def strerror(status: int) -> str:

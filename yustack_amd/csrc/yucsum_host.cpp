@@ -27,6 +27,7 @@
 // grows with the number of concurrent calls the pool allows, not with the
 // number of OS threads that ever called (a Go caller's goroutines migrate over
 // many of them); yu_host_staging_bytes reports it.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -135,39 +136,81 @@ struct Ctx {
     cap_data = cap_pk = 0;
     reserved = false;
   }
-  ~Ctx() {
-    if (dev >= 0 && hipSetDevice(dev) == hipSuccess) release();
+  ~Ctx() { release_on_device(); }
+  // release() with this context's device current (a trim or give-back may run
+  // on a thread whose current device is another one); the caller's device is
+  // restored.
+  void release_on_device() {
+    if (dev < 0) return;
+    int prev = -1;
+    const bool restore = hipGetDevice(&prev) == hipSuccess;
+    if (hipSetDevice(dev) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    release();
+    if (restore && prev != dev) (void)hipSetDevice(prev);
   }
 
+  // Grows the staging to (data_bytes, pk). A failed allocation frees whatever
+  // was allocated before it, so a context is either fully reserved (and its
+  // caps count it) or holds nothing.
   int reserve(uint64_t data_bytes, uint64_t pk) {
     if (data_bytes <= cap_data && pk <= cap_pk) return YU_OK;
     if (data_bytes < cap_data) data_bytes = cap_data;
     if (pk < cap_pk) pk = cap_pk;
     release();
-    reserved = true;  // (partly) allocated: release() frees what a failure left
+    const int rc = allocate(data_bytes, pk);
+    if (rc) {
+      release();
+      return rc;
+    }
+    return YU_OK;
+  }
+
+ private:
+  // Fault injection for the tests (measurement knob, YU_TUNING=1 only):
+  // YU_HOST_FAIL_ALLOC=k makes the k-th staging allocation of the process
+  // (1-based, counted over every context) fail once as out of memory.
+  static hipError_t inject(hipError_t e) {
+    static const long fail_at = [] {
+      const char *v = yu::tuning_env("YU_HOST_FAIL_ALLOC");
+      return v && *v ? strtol(v, nullptr, 10) : 0L;
+    }();
+    static std::atomic<long> count{0};
+    if (fail_at > 0 && e == hipSuccess && ++count == fail_at) return hipErrorOutOfMemory;
+    return e;
+  }
+#define YU_TRY_ALLOC(expr) YU_TRY(inject(expr))
+
+  int allocate(uint64_t data_bytes, uint64_t pk) {
+    // reserved before the first allocation: yu_host_staging_bytes counts a
+    // context whose caps are set, and these are set only once all succeeded
+    reserved = true;
     for (int k = 0; k < nslots; ++k) {
       Slot &x = s[k];
       YU_TRY(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
       YU_TRY(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
-      YU_TRY(hipHostMalloc((void **)&x.h_data, data_bytes ? data_bytes : 16, 0));
-      YU_TRY(hipHostMalloc((void **)&x.h_addrs, pk * 8, 0));
-      YU_TRY(hipHostMalloc((void **)&x.h_init, pk * 2, 0));
+      YU_TRY_ALLOC(hipHostMalloc((void **)&x.h_data, data_bytes ? data_bytes : 16, 0));
+      YU_TRY_ALLOC(hipHostMalloc((void **)&x.h_addrs, pk * 8, 0));
+      YU_TRY_ALLOC(hipHostMalloc((void **)&x.h_init, pk * 2, 0));
       // results: up to 2 per packet (YU_MODE_OUTPUTS)
-      YU_TRY(hipHostMalloc((void **)&x.h_out, pk * 4, 0));
-      YU_TRY(hipHostMalloc((void **)&x.h_off, (pk + 1) * 8, 0));
-      YU_TRY(hipHostMalloc((void **)&x.h_outc, pk * 4, hipHostMallocCoherent));
-      YU_TRY(hipHostMalloc((void **)&x.h_flag, 64, hipHostMallocCoherent));
+      YU_TRY_ALLOC(hipHostMalloc((void **)&x.h_out, pk * 4, 0));
+      YU_TRY_ALLOC(hipHostMalloc((void **)&x.h_off, (pk + 1) * 8, 0));
+      YU_TRY_ALLOC(hipHostMalloc((void **)&x.h_outc, pk * 4, hipHostMallocCoherent));
+      YU_TRY_ALLOC(hipHostMalloc((void **)&x.h_flag, 64, hipHostMallocCoherent));
       *x.h_flag = 0;
-      YU_TRY(hipMalloc((void **)&x.d_data, data_bytes ? data_bytes : 16));
-      YU_TRY(hipMalloc((void **)&x.d_addrs, pk * 8));
-      YU_TRY(hipMalloc((void **)&x.d_init, pk * 2));
-      YU_TRY(hipMalloc((void **)&x.d_out, pk * 4));
-      YU_TRY(hipMalloc((void **)&x.d_off, (pk + 1) * 8));
+      YU_TRY_ALLOC(hipMalloc((void **)&x.d_data, data_bytes ? data_bytes : 16));
+      YU_TRY_ALLOC(hipMalloc((void **)&x.d_addrs, pk * 8));
+      YU_TRY_ALLOC(hipMalloc((void **)&x.d_init, pk * 2));
+      YU_TRY_ALLOC(hipMalloc((void **)&x.d_out, pk * 4));
+      YU_TRY_ALLOC(hipMalloc((void **)&x.d_off, (pk + 1) * 8));
     }
     cap_data = data_bytes;
     cap_pk = pk;
     return YU_OK;
   }
+#undef YU_TRY_ALLOC
 };
 
 // Upper bound on the staging contexts of one device (YU_HOST_CONTEXTS, 1..64,
@@ -212,7 +255,7 @@ class ContextPool {
   // keep at most host_contexts() x their standard budgets between calls.
   void give_back(Ctx *c) {
     const uint64_t cap = c->nslots == kSlots ? kSliceBytes : kDirectMax;
-    if (c->cap_data > cap || c->cap_pk > kSlicePkts) c->release();
+    if (c->cap_data > cap || c->cap_pk > kSlicePkts) c->release_on_device();
     {
       std::lock_guard<std::mutex> l(m_);
       idle_.push_back(c);
@@ -229,10 +272,31 @@ class ContextPool {
       dev += device_bytes(c->cap_data, c->cap_pk, c->nslots);
     }
   }
-  // Frees the staging of every idle context (lent ones are left alone).
+  // Frees the staging of every idle context (lent ones are left alone). Each
+  // context is taken out of the idle list and freed outside the lock (hipFree
+  // and hipHostFree may wait on the device), so a concurrent acquire() can take
+  // any other idle context meanwhile; it is put back and a waiter woken after.
   void trim() {
-    std::lock_guard<std::mutex> l(m_);
-    for (Ctx *c : idle_) c->release();
+    std::vector<Ctx *> todo;
+    {
+      std::lock_guard<std::mutex> l(m_);
+      for (Ctx *c : idle_)
+        if (c->reserved) todo.push_back(c);
+    }
+    for (Ctx *c : todo) {
+      {
+        std::lock_guard<std::mutex> l(m_);
+        auto it = std::find(idle_.begin(), idle_.end(), c);
+        if (it == idle_.end()) continue;  // lent meanwhile: its holder keeps it
+        idle_.erase(it);
+      }
+      c->release_on_device();
+      {
+        std::lock_guard<std::mutex> l(m_);
+        idle_.push_back(c);
+      }
+      cv_.notify_one();
+    }
   }
  private:
   std::mutex m_;
@@ -972,6 +1036,14 @@ extern "C" uint64_t yu_host_staging_bytes(int device, uint64_t *dev_bytes) {
 }
 
 extern "C" int yu_host_contexts(void) { return host_contexts(); }
+
+extern "C" const char *yu_hip_runtime_path(void) {
+  // The address of an imported function, taken in this library, is the
+  // definition its calls go to (through the GOT), interposition included.
+  Dl_info info;
+  if (dladdr((void *)&hipGetDevice, &info) == 0 || !info.dli_fname) return nullptr;
+  return info.dli_fname;
+}
 
 extern "C" int yu_host_staging_trim(int device) {
   if (device < 0 || device >= 64) return YU_ENODEV;

@@ -45,7 +45,8 @@ __host__ __device__ inline uint32_t l4_min(uint32_t proto) {
 
 // Measurement knobs (YU_RAGGED, YU_VARIANT, YU_NT, YU_FILL_WB, YU_RUNS,
 // YU_BLOCKS_PER_CU, YU_SEG_SMALL_BLOCKS, YU_XCD, YU_HOST_COPY_THREADS,
-// YU_HOST_DIRECT_MAX) force kernels, grids and cut-overs for tools/ and the
+// YU_HOST_DIRECT_MAX, and the fault injection YU_HOST_FAIL_ALLOC) force
+// kernels, grids, cut-overs and failures for tools/ and the
 // forced-kernel test runs. They are read only when the process also sets
 // YU_TUNING=1, so a production process that inherits one of them keeps the
 // library's own choices; when the gate is open, each knob that is set is named
