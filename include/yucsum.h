@@ -115,13 +115,18 @@ extern "C" {
 /* Bytes outside the packets' fields are never changed.                  */
 /*                                                                      */
 /* Out of contract (device ragged batches only, whose offsets live in    */
-/* device memory and are not checked here): a packet longer than the     */
-/* mode's limit gets an unspecified value, never a fault or a hang. In a */
-/* fill call with such a packet, the field stores of the packet chunk   */
-/* holding it may land elsewhere in [floor4(data + offsets[0]),          */
-/* data + offsets[n]) instead of in the fields. Validate first when the  */
-/* offsets come from outside (the host forms and the Python front end    */
-/* batch.checksum_ragged(validate=True) do).                             */
+/* device memory and are not checked here): a packet whose offsets       */
+/* decrease, or longer than the mode's limit (YU_MAX_TRANSPORT_LEN;      */
+/* RAW: YU_MAX_RAW_LEN). It gets an unspecified result, never a fault or */
+/* a hang. A fill call never writes a byte outside the checksum fields  */
+/* of in-contract packets: no field of an out-of-contract packet is     */
+/* stored, and the kernels that take 16 to 64 consecutive packets at a  */
+/* time (yu_ragged_fill_variant_n names "k_seg<...>") store none of the */
+/* fields of the group holding one (packets [k*c, k*c + c) for the      */
+/* kernel's group size c), whose results are then unspecified too.     */
+/* Every other packet's result and field are exact. Validate first when */
+/* the offsets come from outside (the host forms and the Python front   */
+/* end batch.checksum_ragged(validate=True) do).                        */
 
 /* ------------------------------------------------------------------ */
 /* Scalar entry points (host CPU, Go-signature drop-ins).             */

@@ -1254,13 +1254,21 @@ def load_reference(root="/root/reference"):
     return it
 
 
-def load_path(root="/root/reference"):
+def load_path(root="/root/reference", checksum=None):
     """Everything from the senders to the checker: the packages above, the buffers and
     route the senders use, the senders themselves (sendUDP, sendTCP /
     sendTCPWithOptions, sendICMPv4, ipv4 endpoint.WritePacket) and checker.go. Only the
-    files that hold them are read; bodies are parsed when first run."""
+    files that hold them are read; bodies are parsed when first run.
+    checksum: (directory, files) of another package checksum to load in place of the
+    reference's, e.g. the cgo shim (bindings/go/checksum): every caller above then
+    resolves `checksum.X` to it, unchanged (the caller supplies the shim's `C.*` stubs)."""
     it = Interp(root)
-    it.load("checksum", ["checksum.go"])
+    if checksum is None:
+        it.load("checksum", ["checksum.go"])
+    else:
+        d, files = checksum
+        assert os.path.basename(os.path.normpath(d)) == "checksum"
+        it.load(os.path.abspath(d), files)
     it.load("seqnum", ["seqnum.go"])
     it.load("buffer", ["view.go", "prependable.go"])
     it.load("types", ["types.go", "route.go", "transport.go", "network.go"])

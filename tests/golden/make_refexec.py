@@ -90,8 +90,11 @@ class LinkStub:
 class Ref:
     """The reference's functions, executed by goexec."""
 
-    def __init__(self):
-        self.it = G.load_path(REF)
+    def __init__(self, it=None):
+        """it: an interpreter from G.load_path; by default the reference's own files
+        (the fixture). tests/test_go_shim_exec.py passes one whose package checksum is
+        the cgo shim, to run these same callers unchanged on it."""
+        self.it = it or G.load_path(REF)
         self.it.watch |= {("checker", "IPv4"), ("checker", "TCP.func")}
         self.link = LinkStub(self.it)
 
@@ -261,8 +264,9 @@ def rnd(rng, n):
     return bytes(rng.getrandbits(8) for _ in range(n))
 
 
-def main() -> None:
-    ref = Ref()
+def build(ref: Ref) -> dict:
+    """The fixture's content, computed by `ref`'s interpreter (seeded: the same inputs
+    on every run)."""
     rng = random.Random(20261016)
     C = O.C()
     out = {"generator": "tests/golden/make_refexec.py: reference Go source executed by tests/golden/goexec.py"}
@@ -483,6 +487,12 @@ def main() -> None:
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (mode, bad[:5], got[bad[:5]], want[bad[:5]])
 
+    return out
+
+
+def main() -> None:
+    out = build(Ref())
+    modes, cs, pseudo, comb, wrap = out["modes"], out["checksum"], out["pseudo"], out["combine"], out["wrap"]
     path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(HERE, "refexec.json")
     with open(path, "w") as f:
         json.dump(out, f, separators=(",", ":"))

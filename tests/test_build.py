@@ -53,9 +53,11 @@ def test_no_scratch_no_spills(resource_usage):
         assert ru.get("VGPRs Spill") == "0", (name, ru)
         # a few wave-uniform values may spill into VGPR lanes (v_writelane, no
         # memory traffic: scratch stays 0 above); never more than a handful
-        # (the most: 9, k_seg's in-place TXW kind with 16-packet chunks, whose
-        # write-back holds one more buffer descriptor)
-        assert int(ru.get("SGPRs Spill", "0")) <= 10, (name, ru)
+        # (the most: 11, k_seg's in-place TXW kind on 4 KiB tiles, a measurement
+        # alternative only YU_RAGGED=seg4 selects, whose write-back holds one more
+        # buffer descriptor and whose chunk check reads the offsets' high dwords;
+        # the default TXW chunks, c16 and c48: 9 and 7)
+        assert int(ru.get("SGPRs Spill", "0")) <= 11, (name, ru)
 
 
 def test_occupancy_floor(resource_usage):

@@ -223,3 +223,57 @@ def test_batch_calls_on_the_gpu(dev, oracle_c):
                       G.GoList([G.Int(int(v), "uint16") for v in init], "[]uint16"), None, out, *devices)
         assert err is None, err
         assert [x.v for x in out.items] == [int(v) for v in want], len(devices)
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "checksum")), reason="the reference is not here")
+def test_reference_callers_unchanged_on_shim():
+    """north_star: header/ipv4.go, header/tcp.go and header/udp.go call the engine
+    unchanged. The reference's own callers — sendUDP (transport/udp/endpoint.go:164-187),
+    sendTCP / sendTCPWithOptions (transport/tcp/connect.go:556-586, :288-322),
+    sendICMPv4 (network/ipv4/icmp.go:36-45) through types.Route and the ipv4 endpoint's
+    WritePacket (network/ipv4/ipv4.go:80-97), the header methods (header/ipv4.go:177-179,
+    header/tcp.go:165-173, header/udp.go:67-75) and checker.IPv4 / checker.TCP
+    (checker/checker.go:25-40,71-99) — run from /root/reference as they are, with
+    package checksum resolved to bindings/go/checksum (checksum.go, batch.go) and its
+    `C.*` names bound to libyucsum. The fixture generator (tests/golden/make_refexec.py)
+    runs on that interpreter with its seeded inputs: every stored field, every checker
+    xsum and every Checksum / PseudoHeaderChecksum / ChecksumCombine vector must equal
+    the committed refexec.json, which the same generator made with the reference's own
+    checksum.go. Payloads of 256 bytes and more cross into C.yu_checksum (counted).
+    Test infrastructure only (the interpreter reads the reference at run time): parity
+    stays unpinned by a Go build."""
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import make_refexec as M
+    it = G.load_path(REF, checksum=(os.path.join(ROOT, "bindings", "go", "checksum"), ["checksum.go", "batch.go"]))
+    stubs = cgo_stubs()
+    calls = {"yu_checksum": 0, "bytes": 0}
+    inner = stubs["C.yu_checksum"]
+
+    def counted(p, n, init):
+        calls["yu_checksum"] += 1
+        calls["bytes"] += n.v
+        return inner(p, n, init)
+    stubs["C.yu_checksum"] = counted
+    it.stubs.update(stubs)
+    # the package the callers resolve is the shim: its own helper exists, the reference's file is not loaded
+    assert "goSum" in it.pkgs["checksum"].funcs and "BatchHostUniform" in it.pkgs["checksum"].funcs
+    got = json.loads(json.dumps(M.build(M.Ref(it))))
+    with open(os.path.join(ROOT, "tests", "golden", "refexec.json")) as f:
+        want = json.load(f)
+    assert got.keys() == want.keys()
+    for key in want:
+        if key == "modes":
+            for mode, vecs in want["modes"].items():
+                assert len(got["modes"][mode]) == len(vecs), mode
+                bad = [i for i, (a, b) in enumerate(zip(got["modes"][mode], vecs)) if a != b]
+                assert not bad, (mode, bad[:5], [got["modes"][mode][i] for i in bad[:2]], [vecs[i] for i in bad[:2]])
+        else:
+            assert got[key] == want[key], key
+    n_exec = sum(1 for vecs in want["modes"].values() for v in vecs if v["src"] == "exec")
+    print(f"{n_exec} executed-caller vectors on the shim; C.yu_checksum: {calls['yu_checksum']} calls, "
+          f"{calls['bytes']} bytes")
+    assert calls["yu_checksum"] > 100 and calls["bytes"] > 100_000, calls

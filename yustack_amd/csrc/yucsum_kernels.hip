@@ -381,7 +381,7 @@ __device__ __forceinline__ uint32_t packet_value(const BatchArgs &A, uint32_t v,
 __device__ __forceinline__ void store_field(const BatchArgs &A, uint32_t r, uint8_t *pkt,
                                             uint32_t hdr_end) {
   const int mode = A.mode;
-  if (A.fill && mode_is_tx(mode)) {
+  if (A.fill && pkt && mode_is_tx(mode)) {
     const uint32_t f = mode_field(mode);
     if (f + 2u <= hdr_end) {
       // binary.BigEndian.PutUint16: one 16-bit store when the field is
@@ -400,6 +400,16 @@ __device__ __forceinline__ void store_field(const BatchArgs &A, uint32_t r, uint
       }
     }
   }
+}
+
+// The packet at `off` whose field a fill call may write: none when not filling,
+// or when its length is out of contract (a ragged packet longer than
+// YU_MAX_TRANSPORT_LEN, or with decreasing offsets, whose length wraps): such a
+// packet gets an unspecified value and no byte is written for it
+// (include/yucsum.h, "Out of contract"). Every fill mode is a transport / IPv4
+// / ICMP / datagram mode, so the limit is the transport one.
+__device__ __forceinline__ uint8_t *fill_at(const BatchArgs &A, uint64_t off, uint64_t len) {
+  return A.fill && len <= YU_MAX_TRANSPORT_LEN ? A.fill + off : nullptr;
 }
 
 __device__ __forceinline__ void finish_packet(const BatchArgs &A, uint64_t p,
@@ -1021,7 +1031,7 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
       if (lead) {
         const uint32_t s = acc - junk_sum<BE>(jx, j, sel);
         const uint32_t v = BE ? s : le_to_be(s, cur.sh & 1u);
-        finish_packet(A, p, v, cur.len, sd, A.fill ? A.fill + cur.soff : nullptr,
+        finish_packet(A, p, v, cur.len, sd, fill_at(A, cur.soff, cur.len),
                       E - cur.sh);
       }
       if (!more) break;
@@ -1122,7 +1132,7 @@ __global__ __launch_bounds__(256) void k_hdr(BatchArgs A) {
       Side sd;
       sd.a = sd.b = 0u;
       sd.i = 0;
-      finish_packet(A, p, v, len, sd, A.fill ? A.fill + s : nullptr, E - sh);
+      finish_packet(A, p, v, len, sd, fill_at(A, s, len), E - sh);
     }
   }
 }
@@ -1287,7 +1297,7 @@ __global__ __launch_bounds__(256) void k_rag(BatchArgs A) {
     const uint64_t so = shfl64(it.o, gw);  // all lanes: a cross-lane read needs active sources
     if (gl == G - 1 && it.fits) {
       const uint32_t v = le_to_be(acc - junk_sum<false>(jx, j, 0u), it.sh & 1u);
-      finish_packet(A, pb + gw, v, it.len, it.sd, A.fill ? A.fill + so : nullptr, E - it.sh);
+      finish_packet(A, pb + gw, v, it.len, it.sd, fill_at(A, so, it.len), E - it.sh);
     }
     if (!more) break;
     it = nx;
@@ -1334,7 +1344,7 @@ __global__ __launch_bounds__(256) void k_rag(BatchArgs A) {
       const uint32_t v = plen > kLEMax ? rag_serial_sum<true>(pabs, E - sh, E, lane, end, pjx, j)
                                        : rag_serial_sum<false>(pabs, E - sh, E, lane, end, pjx, j);
       const Side sd = load_side(sp, p);
-      if (lane == 63) finish_packet(A, p, v, plen, sd, A.fill ? A.fill + ps : nullptr, E - sh);
+      if (lane == 63) finish_packet(A, p, v, plen, sd, fill_at(A, ps, plen), E - sh);
     }
   }
 }
@@ -1413,7 +1423,24 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
 // (the in-place writer's whole-line write-back, k_seg), unless that line begins
 // before the batch; else at its dword. The bytes in front are loaded but lie
 // before every point, and the line was fetched for the previous chunk anyway.
+//
+// Out-of-contract chunks (device ragged batches, whose offsets the host never
+// reads): a packet whose offsets decrease or whose length exceeds lim, the
+// mode's limit (include/yucsum.h).
+//  - The writing kinds (each = true: TX, TXW, DG) test every packet of the
+//    chunk, wave-uniformly, on the offsets already loaded. A chunk holding such
+//    a packet gets xe = 0: it streams nothing (its results are unspecified) and
+//    stores no field (k_seg's epilogue stores only for xe > 0, which loses
+//    nothing: an in-contract chunk with xe == 0 holds only empty packets).
+//    Every other chunk lies back to back from its first offset, each packet
+//    within the limit, so its positions are exact (< 64 x 65536 bytes: the
+//    32-bit positions never wrap).
+//  - The read-only kinds (plain, RX) only bound the chunk's span to what CH
+//    in-contract packets can cover, so a chunk's time is bounded whatever the
+//    offsets say (a decreasing chunk end would wrap xe); a packet out of
+//    contract gets an unspecified result, its neighbours stay exact.
 __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk &k,
+                                         uint32_t, bool ragged, uint32_t lim, bool each, uint32_t ch,
                                          bool line128 = false) {
   if (p0 >= n) {
     k.b0 = data & ~3ull;
@@ -1425,6 +1452,10 @@ __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0,
   const uint64_t l = s & ~127ull;
   k.b0 = line128 && l >= (data & ~3ull) ? l : s & ~3ull;
   k.xe = e - k.b0;
+  // (lanes past the chunk sit at its end: length 0)
+  if (ragged && (each ? __any((int)(k.oy - k.ox > (uint64_t)lim)) != 0
+                      : k.xe > (uint64_t)ch * lim + 131u))  // (+ b0's up to 131 bytes in front)
+    k.xe = 0;
 }
 
 // The TX kind (UDP / TCP / ICMP fields: packets <= 65535 bytes, so a chunk spans
@@ -1438,6 +1469,7 @@ __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0,
 struct SegChunk32 {
   uint32_t ey;  // low dword of this lane's packet end (lanes past the batch or
                 // the chunk: the chunk end)
+  uint32_t eh;  // its high dword (ragged; dead once seg_geom has checked the chunk)
   uint64_t s0;  // the chunk's first offset (ragged: offsets[p0]; uniform: p0 * stride)
   uint64_t b0;  // address the chunk's tiles start at (wave-uniform, see seg_geom)
   uint64_t xe;  // chunk end relative to b0 (wave-uniform)
@@ -1452,16 +1484,19 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
   const uint64_t ce = p0 < n ? (n - p0 < (uint64_t)CH ? n : p0 + CH) : n;
   const bool own = lane < (uint32_t)CH && i < n;
   const uint64_t last = p0 < n ? ce - 1u : 0u;
-  const uint32_t *lo = A.offsets ? (const uint32_t *)A.offsets : g_side_zero;  // little-endian
-  const uint32_t ry = lo[A.offsets ? 2u * (own ? i + 1 : ce) : 0];
   const uint64_t *offs = A.offsets ? A.offsets : (const uint64_t *)g_side_zero;
+  const uint64_t ry = offs[A.offsets ? (own ? i + 1 : ce) : 0];
   const uint64_t r0 = offs[A.offsets ? (p0 < n ? p0 : n) : 0];
-  k.ey = A.offsets ? ry : (uint32_t)((own ? i : last) * A.stride + A.len);
+  k.ey = A.offsets ? (uint32_t)ry : (uint32_t)((own ? i : last) * A.stride + A.len);
+  k.eh = (uint32_t)(ry >> 32);
   k.s0 = A.offsets ? r0 : (p0 < n ? p0 : 0u) * A.stride;
   if (SIDE) k.sd = load_side(sp, own ? i : n - 1);
 }
 
+// (the same checks, on the 64-bit ends: a lane's start is its left neighbour's
+// end, lane 0's the chunk's first offset)
 __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk32 &k,
+                                         uint32_t lane, bool ragged, uint32_t lim, bool, uint32_t,
                                          bool line128 = false) {
   if (p0 >= n) {
     k.b0 = data & ~3ull;
@@ -1475,6 +1510,11 @@ __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0,
   const uint64_t l = s & ~127ull;
   k.b0 = line128 && l >= (data & ~3ull) ? l : s & ~3ull;
   k.xe = (uint64_t)((uint32_t)__builtin_amdgcn_readlane((int)k.ey, 63) - (uint32_t)s0) + (s - k.b0);
+  if (ragged) {
+    const uint64_t ye = ((uint64_t)k.eh << 32) | k.ey;
+    const uint64_t yl = shfl64(ye, lane ? lane - 1u : 0u);
+    if (__any((int)(ye - (lane ? yl : s0) > (uint64_t)lim))) k.xe = 0;
+  }
 }
 
 // This lane's packet as (position relative to b0, length).
@@ -1692,6 +1732,7 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   constexpr bool TXW = K == kSegTxW;
   constexpr bool tx = K == kSegTx || TXW;
   constexpr bool FB = tx || DG;                 // a field whose bytes are read from the tile
+  constexpr bool FILLK = FB;                    // a kind that may write fields (seg_geom)
   constexpr int NP = K == kSegRx || DG ? 4 : 2;  // point slots in use
   constexpr uint32_t T = 64u * 16u * U;
   constexpr uint32_t NC = 64u * U;  // chunks per tile
@@ -1714,6 +1755,9 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   // last tile of each chunk and its whole 128-byte lines are stored back with
   // non-temporal stores. See the chunk epilogue.
   const bool wbk = TXW && A.fill && contig;
+  // a packet's length limit (include/yucsum.h); a chunk holding a longer one is
+  // out of contract (seg_geom). Only the plain kind takes RAW packets.
+  const uint32_t lim = K == kSegPlain && mode == YU_MODE_RAW ? YU_MAX_RAW_LEN : YU_MAX_TRANSPORT_LEN;
   // Positions relative to the chunk's b0: 64-bit for the plain kind (RAW packets
   // up to YU_MAX_RAW_LEN), 32-bit for the TX / RX / DG kinds, whose packets are
   // at most 65535 bytes (include/yucsum.h), so a 64-packet chunk spans < 4.2 MB
@@ -1734,7 +1778,7 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   Chunk cur, nxt;
   seg_load<CH, !RX>(A, sp, ch * CH, lane, cur);
   seg_load<CH, !RX>(A, sp, (ch + nwave) * CH, lane, nxt);
-  seg_geom(data, A.n, ch * CH, cur, wbk);
+  seg_geom(data, A.n, ch * CH, cur, lane, contig, lim, FILLK, CH, wbk);
 
   // per-chunk state
   SegPt<Pos> pt[4];  // start, end, then (RX, DG) header and transport end
@@ -1803,7 +1847,7 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
     Chunk nn;  // the chunk after next: its loads go out before this
                   // step's tile loads, so waiting on them never waits on those
     if (last) {
-      seg_geom(data, A.n, (ch + nwave) * CH, nxt, wbk);
+      seg_geom(data, A.n, (ch + nwave) * CH, nxt, lane, contig, lim, FILLK, CH, wbk);
       seg_load<CH, !RX>(A, sp, (ch + 2u * nwave) * CH, lane, nn);  // (RX, DG: no side data)
     }
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
@@ -2001,8 +2045,11 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
     Pos wq = 0;
     bool wf = false;
     uint32_t wl = 64u, wr = 0u;
+    // an out-of-contract chunk (xe == 0, seg_geom) stores nothing: no field, no line
+    const bool wr_ok = A.fill && cur.xe != 0u;
+    const bool wbc = wbk && cur.xe != 0u;
     Pos x0 = 0;  // the chunk's start (wbk: the TX kind, 32-bit)
-    if (wbk) x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);
+    if (wbc) x0 = (Pos)(uint32_t)__shfl((int)(uint32_t)pt[0].x, 0, 64);
     if (lane < (uint32_t)CH && p < A.n) {
       const uint32_t odd = (uint32_t)pt[0].x & 1u;
       if (DG) {
@@ -2023,7 +2070,7 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
             A.out[2u * p + 1u] = (uint16_t)l4;
           }
         }
-        if (A.fill) {
+        if (wr_ok) {
           uint8_t *pk = A.fill + (cur.b0 + pt[0].x - data);
           if (rx.hl) put_be16(pk + 10u, ip);
           if (rx.fo) put_be16(pk + rx.fo, l4);
@@ -2054,8 +2101,8 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
           v = le_to_be(pe - pt[0].p - (tx ? fsum : 0u), odd);
         }
         const uint64_t len = plen;
-        uint8_t *pk = A.fill ? A.fill + (cur.b0 + pt[0].x - data) : nullptr;
-        if (tx && wbk && park && fld + 2u <= len) {
+        uint8_t *pk = wr_ok ? A.fill + (cur.b0 + pt[0].x - data) : nullptr;
+        if (tx && wbc && park && fld + 2u <= len) {
           // the field's offset in the parked (last) tile, wrapping below it;
           // its line is stored whole below when the field lies in one line of
           // this tile that holds no byte outside this chunk
@@ -2075,7 +2122,7 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
         if (pk) store_field(A, r, pk, (uint32_t)(len < 0xFFFFFFFFu ? len : 0xFFFFFFFFu));
       }
     }
-    if (tx && wbk && park) {  // wave-uniform: the in-place write-back
+    if (tx && wbc && park) {  // wave-uniform: the in-place write-back
       // 1. Every field byte that lies in the tile goes into its parked copy, the
       //    ones left to their 2-byte stores too (same bytes: a line stored whole
       //    that holds one stays right).
@@ -2198,9 +2245,9 @@ __global__ __launch_bounds__(256) void k_loop_rx(BatchArgs A) {
           A.out[2u * p] = (uint16_t)ip;
           A.out[2u * p + 1u] = (uint16_t)l4;
         }
-        if (A.fill) {
-          if (rx.hl) put_be16(A.fill + cur.soff + 10u, ip);
-          if (fo) put_be16(A.fill + cur.soff + fo, l4);
+        if (uint8_t *pk = fill_at(A, cur.soff, cur.len)) {
+          if (rx.hl) put_be16(pk + 10u, ip);
+          if (fo) put_be16(pk + fo, l4);
         }
       } else if (lane == 63u) {
         // header: Checksum(b[:HeaderLength()]) in {0, 0xffff}; transport:
