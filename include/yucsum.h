@@ -118,15 +118,17 @@ extern "C" {
 /* device memory and are not checked here): a packet whose offsets       */
 /* decrease, or longer than the mode's limit (YU_MAX_TRANSPORT_LEN;      */
 /* RAW: YU_MAX_RAW_LEN). It gets an unspecified result, never a fault or */
-/* a hang. A fill call never writes a byte outside the checksum fields  */
-/* of in-contract packets: no field of an out-of-contract packet is     */
-/* stored, and the kernels that take 16 to 64 consecutive packets at a  */
-/* time (yu_ragged_fill_variant_n names "k_seg<...>") store none of the */
-/* fields of the group holding one (packets [k*c, k*c + c) for the      */
-/* kernel's group size c), whose results are then unspecified too.     */
-/* Every other packet's result and field are exact. Validate first when */
-/* the offsets come from outside (the host forms and the Python front   */
-/* end batch.checksum_ragged(validate=True) do).                        */
+/* a hang (for offsets that do not wrap the address space). A kernel     */
+/* that takes a group of consecutive packets at a time (k_seg's chunks  */
+/* of 16 to 64 packets, k_hdr's steps of 64; yu_ragged_variant_n and    */
+/* yu_ragged_fill_variant_n name the kernel) may give the other packets */
+/* of the group holding one, [k*c, k*c + c) for group size c,           */
+/* unspecified results too. A fill call never writes a byte outside the */
+/* checksum fields of in-contract packets: no field of an out-of-       */
+/* contract packet is stored, nor any field of its group. Every other   */
+/* packet's result and field are exact. Validate first when the offsets */
+/* come from outside (the host forms and the Python front end           */
+/* batch.checksum_ragged(validate=True) do).                            */
 
 /* ------------------------------------------------------------------ */
 /* Scalar entry points (host CPU, Go-signature drop-ins).             */

@@ -41,8 +41,11 @@ def _to(dev, a):
 
 def _group(name: str) -> int:
     """Packets per group whose fields a bad packet takes with it: the writing k_seg
-    kinds (tx, txw, dg) check whole chunks; per-packet kernels and the read-only
-    kinds only the packet itself."""
+    kinds (tx, txw, dg) check whole chunks, k_hdr whole 64-packet steps (one buffer
+    descriptor from lane 0's packet); per-packet kernels and the read-only k_seg kinds
+    only the packet itself."""
+    if name == "k_hdr":
+        return 64
     if not name.startswith("k_seg<") or not any(t in name for t in (",tx", ",dg")):
         return 1
     for part in name[6:-1].split(","):

@@ -1269,12 +1269,18 @@ def test_direct_path_back_to_back_bursts(dev, oracle_c):
         assert np.array_equal(got, want), (it, n, L)
 
 
-def test_fill_ragged_ipv4_headers(dev, oracle_c):
+@pytest.mark.parametrize("packed,shift", [(False, 0), (True, 1), (True, 3)])
+def test_fill_ragged_ipv4_headers(dev, oracle_c, packed, shift):
     """Ragged IPv4 TX in place (k_hdr): the header field written big-endian equals
-    the oracle's value, and the filled headers verify (checker.IPv4)."""
-    rng = np.random.default_rng(43)
+    the oracle's value, and the filled headers verify (checker.IPv4). `packed`:
+    lengths as drawn (not rounded to 4) and the batch 1 or 3 bytes past a dword, so
+    fields lie at every address parity: only bytes 10-11 of each header
+    change, and the bytes before the batch stay."""
+    rng = np.random.default_rng(43 + shift)
     n = 3000
-    lens = (rng.integers(20, 1501, size=n) + 3) & ~3
+    lens = rng.integers(20, 1501, size=n)
+    if not packed:
+        lens = (lens + 3) & ~3
     offs = np.zeros(n + 1, np.uint64)
     offs[1:] = np.cumsum(lens)
     blob = _rand(rng, int(offs[-1]))
@@ -1283,13 +1289,22 @@ def test_fill_ragged_ipv4_headers(dev, oracle_c):
         ihl = int(rng.integers(5, 16))
         blob[s] = 0x40 | (ihl if ihl * 4 <= lens[i] else 5)
     want = oracle_c.batch(blob, O.MODE_IPV4, offsets=offs)
-    d = _to(dev, blob)
+    pre = _rand(rng, shift)
+    whole = _to(dev, np.concatenate([pre, blob, np.zeros(16, np.uint8)]))
+    d = whole[shift:]
     got = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), "ipv4", fill=True).cpu().numpy()
     assert np.array_equal(got, want)
-    filled = d.cpu().numpy()
-    fields = (filled[offs[:-1].astype(np.int64) + 10].astype(np.uint16) << 8) | filled[offs[:-1].astype(np.int64) + 11]
-    assert np.array_equal(fields, want)
-    v = batch.checksum_ragged(d, _to(dev, offs.view(np.int64)), "verify_ipv4")
+    filled = d.cpu().numpy()[:blob.size]
+    st = offs[:-1].astype(np.int64)
+    exp = blob.copy()
+    exp[st + 10] = (want >> 8).astype(np.uint8)
+    exp[st + 11] = (want & 0xFF).astype(np.uint8)
+    bad = np.nonzero(filled != exp)[0]
+    assert bad.size == 0, bad[:10]
+    assert np.array_equal(whole[:shift].cpu().numpy(), pre)
+    if packed:
+        assert ((st + 10 + shift) & 1).any() and (((st + 10 + shift) & 1) == 0).any()
+    v = batch.checksum_ragged(d[:blob.size], _to(dev, offs.view(np.int64)), "verify_ipv4")
     assert bool(batch.verified(v).all())
 
 

@@ -1095,6 +1095,11 @@ __global__ __launch_bounds__(256) void k_hdr(BatchArgs A) {
     const uint64_t sa = data + s;
     const uint32_t sh = (uint32_t)sa & 3u;
     const uint64_t len = e - s;
+    // The descriptor starts at lane 0's packet, so one out-of-contract packet of the
+    // step (decreasing offsets, or longer than YU_MAX_TRANSPORT_LEN: include/yucsum.h)
+    // can move every lane's window out of it: such a step stores no field (its
+    // results are unspecified). In contract, lane 0's start is the step's lowest.
+    const bool step_ok = !__any((int)(len > YU_MAX_TRANSPORT_LEN));
     const uint32_t lmax = sh + (uint32_t)(len < 60u ? len : 60u);  // bytes to load
     const uint64_t wo = (sa & ~3ull) - base;
     uint4 c[4];
@@ -1132,7 +1137,7 @@ __global__ __launch_bounds__(256) void k_hdr(BatchArgs A) {
       Side sd;
       sd.a = sd.b = 0u;
       sd.i = 0;
-      finish_packet(A, p, v, len, sd, fill_at(A, s, len), E - sh);
+      finish_packet(A, p, v, len, sd, step_ok ? fill_at(A, s, len) : nullptr, E - sh);
     }
   }
 }
