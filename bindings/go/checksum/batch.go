@@ -175,7 +175,11 @@ func HostStaging(device int) (pinned, dev uint64) {
 // HostContextPinnedMax is the pinned bytes of one bulk and one burst staging
 // context at most, between calls (include/yucsum.h YU_HOST_CONTEXT_PINNED_MAX +
 // YU_HOST_BURST_CONTEXT_PINNED_MAX): HostContexts() of each per device.
-const HostContextPinnedMax = uint64(C.YU_HOST_CONTEXT_PINNED_MAX) + uint64(C.YU_HOST_BURST_CONTEXT_PINNED_MAX)
+// A plain literal, not an expression over the header's macros, which cgo would have
+// to evaluate (the cgo build is unverified here, INTEGRATION.md §2):
+// 3*(32 MiB + 26*2^18 + 72) + (4 MiB + 26*2^18 + 72). tests/test_bindings.py checks it
+// against include/yucsum.h.
+const HostContextPinnedMax uint64 = 132120864
 
 // HostContexts is the bound on staging contexts per device (YU_HOST_CONTEXTS,
 // default 4, read once from the environment).

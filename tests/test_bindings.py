@@ -130,3 +130,19 @@ def test_go_batch_calls_check_side_arrays_and_sizes():
     uni = _func_body(go, "BatchHostUniform")
     assert "(n-1)*stride" not in uni.replace("// overflow-safe form of (n-1)*stride", "")
     assert "/(n-1)" in uni
+
+
+def test_go_literal_constants_match_the_header(tmp_path):
+    """HostContextPinnedMax is a plain integer literal in batch.go (no macro expression
+    for cgo to evaluate): it must equal the header's
+    YU_HOST_CONTEXT_PINNED_MAX + YU_HOST_BURST_CONTEXT_PINNED_MAX, as the C compiler
+    evaluates them."""
+    go = open(os.path.join(GODIR, "batch.go")).read()
+    m = re.search(r"const HostContextPinnedMax uint64 = (\d+)\b", go)
+    assert m, "HostContextPinnedMax is not a literal"
+    src = tmp_path / "c.c"
+    src.write_text('#include <stdio.h>\n#include "yucsum.h"\nint main(void) { printf("%llu", '
+                   "(unsigned long long)(YU_HOST_CONTEXT_PINNED_MAX + YU_HOST_BURST_CONTEXT_PINNED_MAX)); }\n")
+    exe = tmp_path / "c"
+    subprocess.run(["gcc", f"-I{ROOT}/include", str(src), "-o", str(exe)], check=True)
+    assert int(m.group(1)) == int(subprocess.run([str(exe)], capture_output=True, text=True).stdout)

@@ -94,8 +94,6 @@ def cgo_stubs():
     hdr = open(os.path.join(ROOT, "include", "yucsum.h")).read()
     for nm, v in re.findall(r"#define (YU_\w+) \(?(-?(?:0x[0-9A-Fa-f]+|\d+))u?\)?\s", hdr):
         stubs["C." + nm] = G.Int(int(v, 0))
-    stubs["C.YU_HOST_CONTEXT_PINNED_MAX"] = G.Int(_lib.HOST_CONTEXT_PINNED_MAX)
-    stubs["C.YU_HOST_BURST_CONTEXT_PINNED_MAX"] = G.Int(_lib.HOST_BURST_CONTEXT_PINNED_MAX)
     return stubs
 
 
