@@ -116,8 +116,9 @@ extern "C" {
 /*                                                                      */
 /* Out of contract (device ragged batches only, whose offsets live in    */
 /* device memory and are not checked here): a packet whose offsets       */
-/* decrease, or longer than the mode's limit (YU_MAX_TRANSPORT_LEN;      */
-/* RAW: YU_MAX_RAW_LEN). It gets an unspecified result, never a fault or */
+/* decrease, longer than the mode's limit (YU_MAX_TRANSPORT_LEN; RAW:    */
+/* YU_MAX_RAW_LEN), or ending past offsets[n] (a call touches at most    */
+/* data[0, offsets[n])). It gets an unspecified result, never a fault or */
 /* a hang (for offsets that do not wrap the address space). A kernel     */
 /* that takes a group of consecutive packets at a time (k_seg's chunks  */
 /* of 16 to 64 packets, k_hdr's steps of 64; yu_ragged_variant_n and    */

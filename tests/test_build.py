@@ -53,11 +53,13 @@ def test_no_scratch_no_spills(resource_usage):
         assert ru.get("VGPRs Spill") == "0", (name, ru)
         # a few wave-uniform values may spill into VGPR lanes (v_writelane, no
         # memory traffic: scratch stays 0 above); never more than a handful
-        # (the most: 11, k_seg's in-place TXW kind on 4 KiB tiles, a measurement
+        # (the most: 13, k_seg's in-place TXW kind on 4 KiB tiles, a measurement
         # alternative only YU_RAGGED=seg4 selects, whose write-back holds one more
-        # buffer descriptor and whose chunk check reads the offsets' high dwords;
-        # the default TXW chunks, c16 and c48: 9 and 7)
-        assert int(ru.get("SGPRs Spill", "0")) <= 11, (name, ru)
+        # buffer descriptor and whose out-of-contract chunk check reads the offsets'
+        # high dwords and the batch end; the default TXW chunks, c16 and c48: 11 and
+        # 9, reloaded ~10 times per 8 KiB tile: config 13 45.94 -> 45.81 us with the
+        # check, profiles/r06/bench_r06b.json)
+        assert int(ru.get("SGPRs Spill", "0")) <= 13, (name, ru)
 
 
 def test_occupancy_floor(resource_usage):

@@ -17,7 +17,11 @@ Corruptions (seeded, applied to clean batches whose oracle values are known):
         the offsets cannot see);
   long  packet k spans more than 65535 bytes, the packets it swallows are empty;
   down  offsets[k] moved 2 bytes before offsets[k-1] (packet k-1 negative,
-        packet k starts inside packet k-2's tail).
+        packet k starts inside packet k-2's tail);
+  past  packet k moved past offsets[n] (a well-sized packet outside what the call
+        may touch, data[0, offsets[n]); its neighbours' lengths go wrong with it).
+The device buffer has 4 KiB of padding past offsets[n], so a store that escaped
+the batch would land in it (and be seen) rather than outside the allocation.
 """
 import numpy as np
 import pytest
@@ -83,6 +87,8 @@ def _corrupt(rng, offs, kind, sites):
             while int(offs[m]) - int(offs[k]) <= 70000:
                 m += 1
             o[k + 1:m] = offs[m]
+        elif kind == "past":
+            o[k], o[k + 1] = offs[-1] + np.uint64(1000), offs[-1] + np.uint64(1100)
         else:  # down
             o[k] = offs[k - 1] - np.uint64(2)
     return o
@@ -142,7 +148,7 @@ def _run(dev, oracle_c, mode, n, kind, fill, seed):
     c = _group(name)
     s_all, e_all = bad_offs[:-1].astype(np.int64), bad_offs[1:].astype(np.int64)
     ln = e_all - s_all  # (int64: negative for decreasing offsets, ~2^32 for hi32)
-    in_c = (ln >= 0) & (ln <= (0xFFFF0000 if mode == O.MODE_RAW else 65535))
+    in_c = (ln >= 0) & (ln <= (0xFFFF0000 if mode == O.MODE_RAW else 65535)) & (e_all <= int(bad_offs[-1]))
     if c > 1:
         g_bad = np.zeros((n + c - 1) // c, bool)
         np.logical_or.at(g_bad, np.arange(n) // c, ~in_c)
@@ -164,7 +170,8 @@ def _run(dev, oracle_c, mode, n, kind, fill, seed):
             continue
         a = None if addrs is None else addrs[8 * i:8 * i + 8]
         exp_val[i] = oracle_c.batch(blob, mode, offsets=np.array([s_all[i], e_all[i]], np.uint64), addrs=a)
-    d = _to(dev, np.concatenate([blob, np.zeros(64, np.uint8)]))
+    pad = rng.integers(0, 256, size=4096, dtype=np.uint8)
+    d = _to(dev, np.concatenate([blob, pad]))
     got = batch.checksum_ragged(d, _to(dev, bad_offs.view(np.int64)), _NAME[mode],
                                 addrs=None if addrs is None else _to(dev, addrs),
                                 fill=fill, validate=False).cpu().numpy().reshape(n, k_out)
@@ -174,7 +181,7 @@ def _run(dev, oracle_c, mode, n, kind, fill, seed):
     if not fill:
         return name, c
     # every byte outside the clean packets' defined fields is unchanged
-    exp = np.concatenate([blob, np.zeros(64, np.uint8)])
+    exp = np.concatenate([blob, pad])
     owner = {}
     for i in np.nonzero(clean)[0]:
         for pos, v in _fields(mode, blob, int(s_all[i]), int(e_all[i]), [int(x) for x in exp_val[i]]):
@@ -193,7 +200,7 @@ _FILL_CASES = [(O.MODE_UDP, 3000), (O.MODE_UDP, 5000), (O.MODE_UDP, 70000), (O.M
                (O.MODE_TX_DATAGRAM, 70000), (O.MODE_IPV4, 5000)]
 
 
-@pytest.mark.parametrize("kind", ["hi32", "long", "down"])
+@pytest.mark.parametrize("kind", ["hi32", "long", "down", "past"])
 @pytest.mark.parametrize("mode,n", _FILL_CASES)
 def test_fill_out_of_contract_writes_only_clean_fields(dev, oracle_c, mode, n, kind):
     """In place on ragged batches with out-of-contract packets: every clean packet's
@@ -208,7 +215,7 @@ def test_fill_out_of_contract_writes_only_clean_fields(dev, oracle_c, mode, n, k
     print(f"{_NAME[mode]} n={n} {kind}: {name}, group {c}")
 
 
-@pytest.mark.parametrize("kind", ["hi32", "long", "down"])
+@pytest.mark.parametrize("kind", ["hi32", "long", "down", "past"])
 @pytest.mark.parametrize("mode,n", [(O.MODE_RAW, 5000), (O.MODE_RAW, 70000), (O.MODE_UDP, 70000),
                                     (O.MODE_VERIFY_RX, 70000), (O.MODE_RAW, 3000)])
 def test_results_next_to_out_of_contract_packets(dev, oracle_c, mode, n, kind):

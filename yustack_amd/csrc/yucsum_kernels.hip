@@ -402,14 +402,29 @@ __device__ __forceinline__ void store_field(const BatchArgs &A, uint32_t r, uint
   }
 }
 
-// The packet at `off` whose field a fill call may write: none when not filling,
-// or when its length is out of contract (a ragged packet longer than
-// YU_MAX_TRANSPORT_LEN, or with decreasing offsets, whose length wraps): such a
-// packet gets an unspecified value and no byte is written for it
-// (include/yucsum.h, "Out of contract"). Every fill mode is a transport / IPv4
-// / ICMP / datagram mode, so the limit is the transport one.
-__device__ __forceinline__ uint8_t *fill_at(const BatchArgs &A, uint64_t off, uint64_t len) {
-  return A.fill && len <= YU_MAX_TRANSPORT_LEN ? A.fill + off : nullptr;
+// The batch's extent: the call may touch data[0, offsets[n]) (ragged; offsets
+// index the caller's data array), everything for uniform batches (whose geometry
+// the host checked). One scalar load per wave.
+struct Extent {
+  uint64_t hi;
+};
+__device__ __forceinline__ Extent batch_extent(const BatchArgs &A) {
+  Extent e;
+  e.hi = A.offsets ? A.offsets[A.n] : ~0ull;
+  return e;
+}
+
+// The packet [off, off + len) whose field a fill call may write: none when not
+// filling, or when the packet is out of contract: longer than
+// YU_MAX_TRANSPORT_LEN (decreasing offsets wrap its length there too) or ending
+// past offsets[n] (outside what the call may touch: some other packet's offsets
+// decrease). Such a packet gets an unspecified value and no byte is written for
+// it (include/yucsum.h, "Out of contract"). Every fill mode is a transport /
+// IPv4 / ICMP / datagram mode, so the limit is the transport one.
+__device__ __forceinline__ uint8_t *fill_at(const BatchArgs &A, const Extent &x, uint64_t off,
+                                            uint64_t len) {
+  const bool in = len <= YU_MAX_TRANSPORT_LEN && off <= x.hi && len <= x.hi - off;
+  return A.fill && in ? A.fill + off : nullptr;
 }
 
 __device__ __forceinline__ void finish_packet(const BatchArgs &A, uint64_t p,
@@ -983,6 +998,7 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
   const SidePtrs sp = side_ptrs(A);
   const bool lead = lane == 63;
   const uint64_t end = A.offsets ? (uint64_t)(uintptr_t)A.data + A.offsets[A.n] : A.end;
+  const Extent ext = batch_extent(A);
 
   uint64_t p = wave;
   if (p >= A.n) return;
@@ -1031,7 +1047,7 @@ __global__ __launch_bounds__(256) void k_loop(BatchArgs A) {
       if (lead) {
         const uint32_t s = acc - junk_sum<BE>(jx, j, sel);
         const uint32_t v = BE ? s : le_to_be(s, cur.sh & 1u);
-        finish_packet(A, p, v, cur.len, sd, fill_at(A, cur.soff, cur.len),
+        finish_packet(A, p, v, cur.len, sd, fill_at(A, ext, cur.soff, cur.len),
                       E - cur.sh);
       }
       if (!more) break;
@@ -1076,6 +1092,7 @@ __global__ __launch_bounds__(256) void k_hdr(BatchArgs A) {
   const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint64_t data = (uint64_t)(uintptr_t)A.data;
   const bool tx = mode_is_tx(A.mode);
+  const Extent ext = batch_extent(A);
   for (uint64_t p0 = wave * 64u; p0 < A.n; p0 += nwave * 64u) {
     const uint64_t p = p0 + lane;
     const bool act = p < A.n;
@@ -1137,7 +1154,7 @@ __global__ __launch_bounds__(256) void k_hdr(BatchArgs A) {
       Side sd;
       sd.a = sd.b = 0u;
       sd.i = 0;
-      finish_packet(A, p, v, len, sd, step_ok ? fill_at(A, s, len) : nullptr, E - sh);
+      finish_packet(A, p, v, len, sd, step_ok ? fill_at(A, ext, s, len) : nullptr, E - sh);
     }
   }
 }
@@ -1265,6 +1282,7 @@ __global__ __launch_bounds__(256) void k_rag(BatchArgs A) {
   const SidePtrs sp = side_ptrs(A);
   const uint64_t data = (uint64_t)(uintptr_t)A.data;
   const uint64_t end = data + A.offsets[A.n];
+  const Extent ext = batch_extent(A);
 
   uint64_t pb = wave * GPW;
   if (pb >= A.n) return;
@@ -1302,7 +1320,7 @@ __global__ __launch_bounds__(256) void k_rag(BatchArgs A) {
     const uint64_t so = shfl64(it.o, gw);  // all lanes: a cross-lane read needs active sources
     if (gl == G - 1 && it.fits) {
       const uint32_t v = le_to_be(acc - junk_sum<false>(jx, j, 0u), it.sh & 1u);
-      finish_packet(A, pb + gw, v, it.len, it.sd, fill_at(A, so, it.len), E - it.sh);
+      finish_packet(A, pb + gw, v, it.len, it.sd, fill_at(A, ext, so, it.len), E - it.sh);
     }
     if (!more) break;
     it = nx;
@@ -1349,7 +1367,7 @@ __global__ __launch_bounds__(256) void k_rag(BatchArgs A) {
       const uint32_t v = plen > kLEMax ? rag_serial_sum<true>(pabs, E - sh, E, lane, end, pjx, j)
                                        : rag_serial_sum<false>(pabs, E - sh, E, lane, end, pjx, j);
       const Side sd = load_side(sp, p);
-      if (lane == 63) finish_packet(A, p, v, plen, sd, fill_at(A, ps, plen), E - sh);
+      if (lane == 63) finish_packet(A, p, v, plen, sd, fill_at(A, ext, ps, plen), E - sh);
     }
   }
 }
@@ -1431,9 +1449,12 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
 //
 // Out-of-contract chunks (device ragged batches, whose offsets the host never
 // reads): a packet whose offsets decrease or whose length exceeds lim, the
-// mode's limit (include/yucsum.h).
+// mode's limit (include/yucsum.h), or which ends past the batch's end
+// (data + offsets[n], what the call may touch).
 //  - The writing kinds (each = true: TX, TXW, DG) test every packet of the
-//    chunk, wave-uniformly, on the offsets already loaded. A chunk holding such
+//    chunk, wave-uniformly, on the offsets already loaded, and the chunk's end
+//    against the batch's (in-chunk order then puts every packet before it). A
+//    chunk holding such
 //    a packet gets xe = 0: it streams nothing (its results are unspecified) and
 //    stores no field (k_seg's epilogue stores only for xe > 0, which loses
 //    nothing: an in-contract chunk with xe == 0 holds only empty packets).
@@ -1446,7 +1467,7 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
 //    contract gets an unspecified result, its neighbours stay exact.
 __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk &k,
                                          uint32_t, bool ragged, uint32_t lim, bool each, uint32_t ch,
-                                         bool line128 = false) {
+                                         uint64_t end, bool line128 = false) {
   if (p0 >= n) {
     k.b0 = data & ~3ull;
     k.xe = 0;
@@ -1458,7 +1479,7 @@ __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0,
   k.b0 = line128 && l >= (data & ~3ull) ? l : s & ~3ull;
   k.xe = e - k.b0;
   // (lanes past the chunk sit at its end: length 0)
-  if (ragged && (each ? __any((int)(k.oy - k.ox > (uint64_t)lim)) != 0
+  if (ragged && (each ? (__any((int)(k.oy - k.ox > (uint64_t)lim)) != 0 || e > end)
                       : k.xe > (uint64_t)ch * lim + 131u))  // (+ b0's up to 131 bytes in front)
     k.xe = 0;
 }
@@ -1502,7 +1523,7 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
 // end, lane 0's the chunk's first offset)
 __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0, SegChunk32 &k,
                                          uint32_t lane, bool ragged, uint32_t lim, bool, uint32_t,
-                                         bool line128 = false) {
+                                         uint64_t end, bool line128 = false) {
   if (p0 >= n) {
     k.b0 = data & ~3ull;
     k.xe = 0;
@@ -1518,7 +1539,8 @@ __device__ __forceinline__ void seg_geom(uint64_t data, uint64_t n, uint64_t p0,
   if (ragged) {
     const uint64_t ye = ((uint64_t)k.eh << 32) | k.ey;
     const uint64_t yl = shfl64(ye, lane ? lane - 1u : 0u);
-    if (__any((int)(ye - (lane ? yl : s0) > (uint64_t)lim))) k.xe = 0;
+    const uint64_t c1 = readlane64(ye, 63);  // the chunk end
+    if (__any((int)(ye - (lane ? yl : s0) > (uint64_t)lim)) || data + c1 > end) k.xe = 0;
   }
 }
 
@@ -1783,7 +1805,7 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
   Chunk cur, nxt;
   seg_load<CH, !RX>(A, sp, ch * CH, lane, cur);
   seg_load<CH, !RX>(A, sp, (ch + nwave) * CH, lane, nxt);
-  seg_geom(data, A.n, ch * CH, cur, lane, contig, lim, FILLK, CH, wbk);
+  seg_geom(data, A.n, ch * CH, cur, lane, contig, lim, FILLK, CH, end, wbk);
 
   // per-chunk state
   SegPt<Pos> pt[4];  // start, end, then (RX, DG) header and transport end
@@ -1852,7 +1874,7 @@ __global__ __launch_bounds__(256, K == kSegDg ? 3 : 1) void k_seg(BatchArgs A) {
     Chunk nn;  // the chunk after next: its loads go out before this
                   // step's tile loads, so waiting on them never waits on those
     if (last) {
-      seg_geom(data, A.n, (ch + nwave) * CH, nxt, lane, contig, lim, FILLK, CH, wbk);
+      seg_geom(data, A.n, (ch + nwave) * CH, nxt, lane, contig, lim, FILLK, CH, end, wbk);
       seg_load<CH, !RX>(A, sp, (ch + 2u * nwave) * CH, lane, nn);  // (RX, DG: no side data)
     }
     seg_fetch<U, NT != 0>(last ? nxt.b0 : cur.b0, last ? nxt.xe : cur.xe, last ? 0u : t + 1u, lane,
@@ -2185,6 +2207,7 @@ __global__ __launch_bounds__(256) void k_loop_rx(BatchArgs A) {
   const uint64_t wave = grid_wave(A.xcd);
   const uint64_t nwave = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint64_t end = A.offsets ? (uint64_t)(uintptr_t)A.data + A.offsets[A.n] : A.end;
+  const Extent ext = batch_extent(A);
 
   uint64_t p = wave;
   if (p >= A.n) return;
@@ -2250,7 +2273,7 @@ __global__ __launch_bounds__(256) void k_loop_rx(BatchArgs A) {
           A.out[2u * p] = (uint16_t)ip;
           A.out[2u * p + 1u] = (uint16_t)l4;
         }
-        if (uint8_t *pk = fill_at(A, cur.soff, cur.len)) {
+        if (uint8_t *pk = fill_at(A, ext, cur.soff, cur.len)) {
           if (rx.hl) put_be16(pk + 10u, ip);
           if (fo) put_be16(pk + fo, l4);
         }
