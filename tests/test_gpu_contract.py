@@ -76,10 +76,10 @@ def _clean_batch(rng, mode, n):
     return blob, offs
 
 
-def _corrupt(rng, offs, kind, sites):
-    """Corrupted copy of offs (uint64) at the given packet indices."""
+def _corrupt(rng, offs, kinds, sites):
+    """Corrupted copy of offs (uint64) at the given packet indices, one kind each."""
     o = offs.copy()
-    for k in sites:
+    for kind, k in zip(kinds, sites):
         if kind == "hi32":
             o[k] += np.uint64(1 << 32)
         elif kind == "long":  # packet k swallows its successors until it passes 65535 bytes
@@ -89,6 +89,8 @@ def _corrupt(rng, offs, kind, sites):
             o[k + 1:m] = offs[m]
         elif kind == "past":
             o[k], o[k + 1] = offs[-1] + np.uint64(1000), offs[-1] + np.uint64(1100)
+        elif kind == "rand":  # anywhere from just past the batch to 2^40 bytes further
+            o[k] = offs[-1] + np.uint64(int(rng.integers(1, 1 << 40)))
         else:  # down
             o[k] = offs[k - 1] - np.uint64(2)
     return o
@@ -118,7 +120,8 @@ def _fields(mode, blob, s, e, vals):
     return out
 
 
-def _run(dev, oracle_c, mode, n, kind, fill, seed):
+def _run(dev, oracle_c, mode, n, kind, fill, seed, nsites=None):
+    """kind: one corruption for every site, or a list (site i takes kinds[i])."""
     rng = np.random.default_rng(seed)
     blob, offs = _clean_batch(rng, mode, n)
     k_out = 2 if mode == O.MODE_TX_DATAGRAM else 1
@@ -131,19 +134,27 @@ def _run(dev, oracle_c, mode, n, kind, fill, seed):
     # written). The writing kinds also get k = 3840, a chunk edge for every chunk size
     # (16, 40, 48, 64), where a chunk's first offset is the corrupt one.
     lens = np.diff(offs.astype(np.int64))
+    nsites = nsites or (1 if n <= 4096 else 3)
+    kinds = [kind] * nsites if isinstance(kind, str) else list(kind)
     cand = np.arange(8, n - 1000)
     if not fill:
         cand = cand[cand % 16 == 5]
-    if kind == "down":
-        cand = cand[lens[cand - 2] >= 16]
-    nsites = 1 if n <= 4096 else 3
-    sites = [3840] if fill and n > 4096 and (kind != "down" or lens[3838] >= 16) else []
-    while len(sites) < nsites:  # >= 1000 packets apart (a long packet swallows <= ~900)
+    sites = []
+    if fill and 3840 < n - 1000 and (kinds[0] != "down" or lens[3838] >= 16):
+        sites = [3840]
+    for _ in range(20000):  # >= 1000 packets apart (a long packet swallows <= ~900)
+        if len(sites) == nsites:
+            break
         k = int(rng.choice(cand))
+        if kinds[len(sites)] == "down" and lens[k - 2] < 16:
+            continue
         if all(abs(k - x) >= 1000 for x in sites):
             sites.append(k)
-    sites = sorted(sites)
-    bad_offs = _corrupt(rng, offs, kind, sites)
+    nsites = len(sites)  # (random placement may fit fewer than asked)
+    kinds = kinds[:nsites]
+    order = np.argsort(sites)
+    sites, kinds = [sites[i] for i in order], [kinds[i] for i in order]
+    bad_offs = _corrupt(rng, offs, kinds, sites)
     name = batch.ragged_variant(_NAME[mode], n, fill=fill)
     c = _group(name)
     s_all, e_all = bad_offs[:-1].astype(np.int64), bad_offs[1:].astype(np.int64)
@@ -157,7 +168,7 @@ def _run(dev, oracle_c, mode, n, kind, fill, seed):
         clean = in_c
     same = (s_all == offs[:-1].astype(np.int64)) & (e_all == offs[1:].astype(np.int64))
     # (a RAW packet past 65535 bytes is in contract: `long` then only moves packets)
-    assert ((~in_c).sum() >= nsites or (mode == O.MODE_RAW and kind == "long")) and clean.mean() > 0.7, (
+    assert ((~in_c).sum() >= nsites or (mode == O.MODE_RAW and "long" in kinds)) and clean.mean() > 0.7, (
         name, (~in_c).sum(), clean.mean())
 
     # expected results of the clean packets: the clean batch's, or (moved packets) the
@@ -177,7 +188,7 @@ def _run(dev, oracle_c, mode, n, kind, fill, seed):
                                 fill=fill, validate=False).cpu().numpy().reshape(n, k_out)
     torch.cuda.synchronize()
     badv = np.nonzero(check & (got != exp_val).any(axis=1))[0]
-    assert badv.size == 0, (name, kind, sites, badv[:10])
+    assert badv.size == 0, (name, kinds, sites, badv[:10])
     if not fill:
         return name, c
     # every byte outside the clean packets' defined fields is unchanged
@@ -190,7 +201,7 @@ def _run(dev, oracle_c, mode, n, kind, fill, seed):
             exp[pos] = v
     filled = d.cpu().numpy()
     diff = np.nonzero(filled != exp)[0]
-    assert diff.size == 0, (name, kind, sites, diff[:10], [owner.get(int(x)) for x in diff[:10]])
+    assert diff.size == 0, (name, kinds, sites, diff[:10], [owner.get(int(x)) for x in diff[:10]])
     return name, c
 
 
@@ -227,3 +238,32 @@ def test_results_next_to_out_of_contract_packets(dev, oracle_c, mode, n, kind):
         pytest.skip("a moved start leaves the datagram contract")
     name, c = _run(dev, oracle_c, mode, n, kind, False, 7300 + 17 * mode + n + len(kind))
     print(f"{_NAME[mode]} n={n} {kind}: {name}, group {c}")
+
+
+def test_out_of_contract_fuzz(dev, oracle_c):
+    """Seeded: 16 batches (YU_CONTRACT_FUZZ_ITERS) of 1100 to 80000 packets, every
+    mode that has a ragged kernel (and its in-place form where it has one), 1 to 4
+    sites each with a random
+    corruption among hi32 / long / down / past / rand (rand: offsets[k] anywhere from
+    just past the batch to 2^40 bytes beyond). Same checks as above: clean packets
+    exact, no byte outside their fields changed, nothing written into the padding."""
+    import os
+    rng = np.random.default_rng(int(os.environ.get("YU_CONTRACT_FUZZ_SEED", "7500")))
+    iters = int(os.environ.get("YU_CONTRACT_FUZZ_ITERS", "16"))
+    modes = [O.MODE_RAW, O.MODE_UDP, O.MODE_TCP, O.MODE_ICMP, O.MODE_IPV4, O.MODE_VERIFY_RX,
+             O.MODE_TX_DATAGRAM]
+    seen = set()
+    for it in range(iters):
+        mode = modes[int(rng.integers(0, len(modes)))]
+        fill = mode not in (O.MODE_RAW, O.MODE_VERIFY_RX) and bool(rng.integers(0, 2))
+        n = int(rng.choice([1100, 3000, 4096, 4097, 9000, 30000, 65536, 80000]))
+        # (sites >= 1000 packets apart in [8, n - 1000))
+        nsites = int(rng.integers(1, min(4, 1 + (n - 1008) // 1000) + 1))
+        allowed = ["hi32", "past", "rand"] + (["long"] if n >= 2100 else [])
+        if mode not in (O.MODE_TCP, O.MODE_TX_DATAGRAM, O.MODE_VERIFY_RX):
+            allowed.append("down")
+        kinds = [allowed[int(rng.integers(0, len(allowed)))] for _ in range(nsites)]
+        name, c = _run(dev, oracle_c, mode, n, kinds, fill, int(rng.integers(0, 1 << 30)), nsites=nsites)
+        seen.add(name)
+        print(f"{it}: {_NAME[mode]} n={n} fill={fill} {kinds}: {name}, group {c}")
+    assert len(seen) >= 6, seen
