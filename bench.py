@@ -750,16 +750,22 @@ def spawn_ranks(plan: dict, argv: list) -> int:
                 if q.poll() is None:
                     q.terminate()
 
+    # The handler only records the signal and sends SIGTERM to the ranks; the loop
+    # below reaps them (SIGKILL after STOP_GRACE_S) and returns 128 + signum. Waiting
+    # inside the handler could block on a Popen lock the interrupted loop holds, and
+    # printing could re-enter sys.stderr's buffer while the loop is writing a log line
+    # (a RuntimeError that used to end the launcher and orphan its ranks), so the
+    # handler writes its note with one unbuffered os.write.
+    got = [0]
+
     def on_signal(signum, _frame):
-        log(f"bench: launcher got signal {signum}; stopping the ranks")
-        stop_all()
-        for q in procs:
+        if not got[0]:
+            got[0] = signum
             try:
-                q.wait(STOP_GRACE_S)
-            except subprocess.TimeoutExpired:
-                q.kill()
-                q.wait()
-        sys.exit(128 + signum)
+                os.write(2, f"bench: launcher got signal {signum}; stopping the ranks\n".encode())
+            except OSError:
+                pass
+        stop_all()
 
     prev = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
     try:
@@ -785,7 +791,7 @@ def spawn_ranks(plan: dict, argv: list) -> int:
                 for q in live:
                     q.kill()
             time.sleep(0.05)
-        return rc
+        return 128 + got[0] if got[0] else rc
     finally:
         for sig, h in prev.items():
             signal.signal(sig, h)

@@ -199,7 +199,8 @@ def test_signal_to_launcher_stops_its_ranks():
     pids = _rank_pids(p, 2)
     assert all(_alive(x) for x in pids)
     p.send_signal(signal.SIGTERM)
-    assert p.wait(30) == 128 + signal.SIGTERM
+    rc = p.wait(30)
+    assert rc == 128 + signal.SIGTERM, (rc, p.stderr.read()[:3000])
     assert not any(_alive(x) for x in pids)  # stopped and reaped by the launcher
 
 
