@@ -266,4 +266,5 @@ def test_out_of_contract_fuzz(dev, oracle_c):
         name, c = _run(dev, oracle_c, mode, n, kinds, fill, int(rng.integers(0, 1 << 30)), nsites=nsites)
         seen.add(name)
         print(f"{it}: {_NAME[mode]} n={n} fill={fill} {kinds}: {name}, group {c}")
-    assert len(seen) >= 6, seen
+    forced = os.environ.get("YU_TUNING") == "1" and bool(os.environ.get("YU_RAGGED"))
+    assert forced or len(seen) >= 6, seen  # (a forced ragged kernel narrows the choice)
