@@ -119,8 +119,11 @@ extern "C" {
 /* decrease, longer than the mode's limit (YU_MAX_TRANSPORT_LEN; RAW:    */
 /* YU_MAX_RAW_LEN), or ending past offsets[n] (a call touches at most    */
 /* data[0, offsets[n])). It gets an unspecified result, never a fault or */
-/* a hang (for offsets that do not wrap the address space). A kernel     */
-/* that takes a group of consecutive packets at a time (k_seg's chunks  */
+/* a hang: every byte a ragged call reads or writes lies in the dwords   */
+/* holding data[0, offsets[n]), whatever the other offsets say           */
+/* (offsets[n] itself must be right, and data + offsets[i] must not wrap */
+/* the address space). A kernel that takes a group of consecutive        */
+/* packets at a time (k_seg's chunks                                    */
 /* of 16 to 64 packets, k_hdr's steps of 64; yu_ragged_variant_n and    */
 /* yu_ragged_fill_variant_n name the kernel) may give the other packets */
 /* of the group holding one, [k*c, k*c + c) for group size c,           */

@@ -1107,7 +1107,10 @@ __global__ __launch_bounds__(256) void k_hdr(BatchArgs A) {
     // wave-uniform descriptor over the 64 packets' bytes (lane 0's start to
     // lane 63's end, which is the chunk's end: lanes past the batch sit there)
     const uint64_t base = uniform64((data + s) & ~3ull);
-    const uint64_t cend = data + readlane64(e, 63);
+    // (clamped to the batch's end: out-of-contract offsets never widen what the
+    // step may read past data[0, offsets[n]))
+    const uint64_t le = readlane64(e, 63);
+    const uint64_t cend = data + (le < ext.hi ? le : ext.hi);
     const __amdgpu_buffer_rsrc_t r = rsrc_at(base, cend);
     const uint64_t sa = data + s;
     const uint32_t sh = (uint32_t)sa & 3u;
