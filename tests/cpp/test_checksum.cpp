@@ -19,6 +19,7 @@
 #include <atomic>
 #include <random>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -332,6 +333,39 @@ static void test_gpu_batches() {
            "device staging %lu within the pool bound", (unsigned long)st.device);
     batch::HostStagingTrim(0);
     EXPECT(batch::HostStaging(0).pinned == 0, "trim frees the idle staging");
+
+    // trims from another thread while calls run: ContextPool::trim takes each idle
+    // context out of the pool and frees it outside the pool's lock, with the
+    // context's device current; callers meanwhile take other contexts or wait
+    std::atomic<bool> done{false};
+    std::atomic<int> trims{0};
+    std::thread trimmer([&] {
+      while (!done) {
+        batch::HostStagingTrim(0);
+        ++trims;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      }
+    });
+    std::vector<std::thread> ts2;
+    for (int t = 0; t < 8; ++t)
+      ts2.emplace_back([&, t] {
+        std::vector<uint16_t> o(bn);
+        for (int r = 0; r < 4; ++r) {
+          const uint64_t k = (t + r) % 2 ? bn : 64;
+          try {
+            batch::HostUniform(big.data(), L, (uint32_t)L, k, batch::RAW, o.data());
+          } catch (const Error &) {
+            ++bad;
+            continue;
+          }
+          if (!std::equal(o.begin(), o.begin() + k, want.begin())) ++bad;
+        }
+      });
+    for (auto &th : ts2) th.join();
+    done = true;
+    trimmer.join();
+    EXPECT(bad == 0 && trims > 0, "8 threads of host calls under concurrent trims (%d trims): %d bad calls",
+           trims.load(), bad.load());
   }
 
   bool threw = false;
