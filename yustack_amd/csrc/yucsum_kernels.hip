@@ -1457,10 +1457,10 @@ __device__ __forceinline__ void seg_load(const BatchArgs &A, const SidePtrs &sp,
 //  - The writing kinds (each = true: TX, TXW, DG) test every packet of the
 //    chunk, wave-uniformly, on the offsets already loaded, and the chunk's end
 //    against the batch's (in-chunk order then puts every packet before it). A
-//    chunk holding such
-//    a packet gets xe = 0: it streams nothing (its results are unspecified) and
-//    stores no field (k_seg's epilogue stores only for xe > 0, which loses
-//    nothing: an in-contract chunk with xe == 0 holds only empty packets).
+//    chunk holding such a packet gets xe = 0: it streams nothing (its results
+//    are unspecified) and stores no field (k_seg's epilogue stores only for
+//    xe > 0, which loses nothing: an in-contract chunk with xe == 0 holds only
+//    empty packets).
 //    Every other chunk lies back to back from its first offset, each packet
 //    within the limit, so its positions are exact (< 64 x 65536 bytes: the
 //    32-bit positions never wrap).
